@@ -1,0 +1,103 @@
+"""Native build of the framework (no setuptools / no hipify / no JIT cache).
+
+Two shared libraries are produced IN-TREE under ``lib/`` so they travel with
+the repository snapshot to the GPU box:
+
+* ``libsvdj_cpu.so`` -- host C++/OpenMP: schedules, CPU oracle, reference
+  input generator, verification (g++).
+* ``libsvdj_hip.so`` -- HIP kernels for gfx950 (CDNA4) + their host drivers
+  (hipcc --offload-arch=gfx950).  Compiles on a CPU-only machine.
+
+Reference parity: replaces the reference's CMake/nvcc build
+(reference CMakeLists.txt:1-26, build/runSVDMPICUDAWithoutCMake.slurm:26).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "lib"
+ARCH = os.environ.get("SVDJ_OFFLOAD_ARCH", "gfx950")
+
+CPU_SOURCES = sorted((CSRC / "cpu").glob("*.cpp"))
+HIP_SOURCES = sorted((CSRC / "hip").glob("*.hip"))
+HEADERS = sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "hip").glob("*.hpp"))
+
+CPU_LIB = LIBDIR / "libsvdj_cpu.so"
+HIP_LIB = LIBDIR / "libsvdj_hip.so"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise FileNotFoundError("hipcc not found (set HIPCC)")
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print("[svdj-build]", " ".join(str(c) for c in cmd), flush=True)
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_cpu(force: bool = False, verbose: bool = False) -> Path:
+    LIBDIR.mkdir(exist_ok=True)
+    if not force and not _stale(CPU_LIB, CPU_SOURCES + HEADERS + [Path(__file__)]):
+        return CPU_LIB
+    cxx = os.environ.get("CXX", "g++")
+    tmp = CPU_LIB.with_suffix(".so.tmp")
+    cmd = [cxx, "-O3", "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-Wall",
+           f"-I{CSRC / 'include'}", *CPU_SOURCES, "-o", tmp]
+    _run(cmd, verbose)
+    os.replace(tmp, CPU_LIB)
+    return CPU_LIB
+
+
+def build_hip(force: bool = False, verbose: bool = False, jobs: int = 4) -> Path:
+    LIBDIR.mkdir(exist_ok=True)
+    if not force and not _stale(HIP_LIB, HIP_SOURCES + HEADERS + [Path(__file__)]):
+        return HIP_LIB
+    hipcc = _hipcc()
+    objdir = LIBDIR / "obj"
+    objdir.mkdir(exist_ok=True)
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+             "-Wno-unused-result", f"-I{CSRC / 'include'}", f"-I{CSRC / 'hip'}"]
+    objs = []
+
+    def compile_one(src: Path):
+        obj = objdir / (src.stem + ".o")
+        if force or _stale(obj, [src] + HEADERS + [Path(__file__)]):
+            _run([hipcc, *flags, "-c", src, "-o", obj], verbose)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, HIP_SOURCES))
+    tmp = HIP_LIB.with_suffix(".so.tmp")
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp], verbose)
+    os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False) -> dict:
+    return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose))}
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    print(build_all(force=force, verbose=True))

@@ -1,0 +1,93 @@
+"""Solver configuration.
+
+The reference's knobs are compile-time macros and hard-coded constants
+(TOLERANCE 1e-16 lib/global.cuh:9, maxIterations = 1 main.cu:482, 16-thread
+blocks main.cu:449, 36 OpenMP threads main.cu:1431, seed 1000000
+main.cu:1445).  Here they are one dataclass, settable from the CLI
+(:func:`add_cli_args`) or environment-free Python.
+"""
+from __future__ import annotations
+
+import argparse
+import enum
+from dataclasses import dataclass, field, asdict
+
+import torch
+
+
+class SVDOptions(enum.IntEnum):
+    """LAPACK-style job options (reference enum SVD_OPTIONS, main.cu:157-161)."""
+
+    AllVec = 0
+    SomeVec = 1
+    NoVec = 2
+
+    @classmethod
+    def parse(cls, v) -> "SVDOptions":
+        if isinstance(v, SVDOptions):
+            return v
+        if isinstance(v, int):
+            return SVDOptions(v)
+        s = str(v).strip().lower()
+        table = {"a": cls.AllVec, "all": cls.AllVec, "allvec": cls.AllVec,
+                 "s": cls.SomeVec, "some": cls.SomeVec, "somevec": cls.SomeVec,
+                 "n": cls.NoVec, "none": cls.NoVec, "novec": cls.NoVec, "o": cls.AllVec}
+        if s not in table:
+            raise ValueError(f"bad SVD option {v!r}")
+        return table[s]
+
+
+_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "fp64": torch.float64,
+           "float64": torch.float64}
+
+
+@dataclass
+class SolverConfig:
+    method: str = "auto"            # auto | block | scalar | oracle
+    dtype: torch.dtype | None = None  # compute dtype (None: input dtype if fp32/fp64)
+    block: int | None = None        # block width W (block path); None: auto
+    tol: float | None = None        # rotation threshold; None: 4 sqrt(m) eps
+    tol_mode: str = "relative"      # relative | absolute (reference parity)
+    max_sweeps: int = 60            # reference: 1 (main.cu:482)
+    max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)
+    ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
+    sort: bool = False              # reference returns unsorted sigma
+    use_graph: bool = False
+    num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
+    checkpoint_dir: str | None = None
+    checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
+    extra: dict = field(default_factory=dict)
+
+    def resolved_dtype(self, A: torch.Tensor) -> torch.dtype:
+        if self.dtype is not None:
+            return self.dtype
+        return A.dtype if A.dtype in (torch.float32, torch.float64) else torch.float32
+
+    def to_dict(self) -> dict:
+        d = asdict(self)
+        d["dtype"] = str(self.dtype) if self.dtype is not None else None
+        return d
+
+
+def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    p.add_argument("--method", default="auto", choices=["auto", "block", "scalar", "oracle"])
+    p.add_argument("--dtype", default=None, choices=sorted(_DTYPES))
+    p.add_argument("--block", type=int, default=None)
+    p.add_argument("--tol", type=float, default=None)
+    p.add_argument("--tol-mode", default="relative", choices=["relative", "absolute"])
+    p.add_argument("--max-sweeps", type=int, default=60)
+    p.add_argument("--max-inner-sweeps", type=int, default=1)
+    p.add_argument("--ordering", default="sameh", choices=["sameh", "round_robin"])
+    p.add_argument("--sort", action="store_true")
+    p.add_argument("--graph", action="store_true")
+    p.add_argument("--checkpoint-dir", default=None)
+    p.add_argument("--checkpoint-every", type=int, default=0)
+    return p
+
+
+def config_from_args(a) -> SolverConfig:
+    return SolverConfig(method=a.method, dtype=_DTYPES[a.dtype] if a.dtype else None,
+                        block=a.block, tol=a.tol, tol_mode=a.tol_mode, max_sweeps=a.max_sweeps,
+                        max_inner_sweeps=a.max_inner_sweeps, ordering=a.ordering, sort=a.sort,
+                        use_graph=a.graph, checkpoint_dir=a.checkpoint_dir,
+                        checkpoint_every=a.checkpoint_every)

@@ -1,0 +1,670 @@
+// Block one-sided Jacobi step on MFMA (the performance path).
+//
+// The reference rotates one column pair at a time with a memory-bound Givens
+// kernel (reference main.cu:139-147) driven by host dot products
+// (main.cu:698-707).  On CDNA4 the same sweep is re-blocked so every byte of
+// A and V moved through HBM feeds matrix-core work:
+//
+//   columns are grouped in blocks of W; a step processes P disjoint block
+//   pairs (bi, bj) with X = [A_bi A_bj] (m x 2W):
+//     gram  : C = A_bi^T A_bj (cross) or G = X^T X (full), MFMA, split over
+//             rows into partial slabs (deterministic, no float atomics);
+//     evd   : G = [[D_bi, C], [C^T, D_bj]] -> Q^T G Q = Lambda by cyclic
+//             parallel Jacobi held entirely in LDS (one 1024-thread WG per
+//             pair); the convergence value max|g_pq|/sqrt(g_pp g_qq) of the
+//             reference (main.cu:710) becomes the stop test;
+//     apply : X <- X Q and [V_bi V_bj] <- [..] Q in place, MFMA, computed
+//             transposed (Out^T = Q^T X^T) so loads AND stores are
+//             128-byte coalesced column segments.
+//
+// Blocks are kept internally orthogonal (every step fully diagonalises its
+// pair), so only the W x W cross Gram is needed per step; the diagonal blocks
+// are the tracked squared column norms D.  The first step of a sweep uses the
+// full Gram, which re-measures every within-block angle from the data.
+#include "common.hpp"
+#include "svdj_hip.h"
+
+#include <cstring>
+#include <vector>
+
+namespace svdj {
+
+constexpr int kGramThreads = 256;
+constexpr int kApplyThreads = 256;
+
+__host__ __device__ constexpr int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// ------------------------------------------------------------------- gram
+template <typename T, int W, bool FULL>
+__global__ __launch_bounds__(kGramThreads) void gram_kernel(
+    const T* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
+    int rows_per_chunk, T* __restrict__ slabs) {
+  using M = Mfma<T>;
+  constexpr int TL = M::TILE;
+  constexpr int HT = W / TL;      // column tiles per block
+  constexpr int NCT = 2 * HT;     // column tiles in X
+  constexpr int NTP = FULL ? NCT * (NCT + 1) / 2 : HT * HT;
+  constexpr int LPL = M::LPL;
+  constexpr int SLAB = FULL ? 4 * W * W : W * W;
+  constexpr int WAVES = kGramThreads / SVDJ_WAVE;
+
+  const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(m_pad, r_begin + rows_per_chunk);
+
+  // tile-pair list (compile-time)
+  typename M::acc_t acc[NTP];
+#pragma unroll
+  for (int i = 0; i < NTP; ++i) acc[i] = M::zero();
+
+  const T* colp[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int blk = ct < HT ? bi : bj;
+    const int col = blk * W + (ct % HT) * TL + M::lane_col(lane);
+    colp[ct] = A + (size_t)col * lda + M::lane_kg(lane) * LPL;
+  }
+
+  for (int r0 = r_begin + wave * 32; r0 < r_end; r0 += WAVES * 32) {
+    T v[NCT][LPL];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) load_col64B<T>(colp[ct] + r0, v[ct]);
+#pragma unroll
+    for (int t = 0; t < LPL; ++t) {
+      int idx = 0;
+      if constexpr (FULL) {
+#pragma unroll
+        for (int a = 0; a < NCT; ++a)
+#pragma unroll
+          for (int b = a; b < NCT; ++b) {
+            acc[idx] = M::mfma(v[a][t], v[b][t], acc[idx]);
+            ++idx;
+          }
+      } else {
+#pragma unroll
+        for (int a = 0; a < HT; ++a)
+#pragma unroll
+          for (int b = 0; b < HT; ++b) {
+            acc[idx] = M::mfma(v[a][t], v[HT + b][t], acc[idx]);
+            ++idx;
+          }
+      }
+    }
+  }
+
+  // Combine the waves' partial tiles in LDS (sequentially, deterministic).
+  __shared__ T red[SLAB];
+  for (int i = threadIdx.x; i < SLAB; i += kGramThreads) red[i] = T(0);
+  __syncthreads();
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+      int idx = 0;
+      if constexpr (FULL) {
+        constexpr int N = 2 * W;
+#pragma unroll
+        for (int a = 0; a < NCT; ++a)
+#pragma unroll
+          for (int b = a; b < NCT; ++b) {
+#pragma unroll
+            for (int e = 0; e < M::NACC; ++e) {
+              const int r = a * TL + M::acc_row(e, lane);
+              const int c = b * TL + M::lane_col(lane);
+              red[r * N + c] += acc[idx][e];
+              if (a != b) red[c * N + r] += acc[idx][e];
+            }
+            ++idx;
+          }
+      } else {
+#pragma unroll
+        for (int a = 0; a < HT; ++a)
+#pragma unroll
+          for (int b = 0; b < HT; ++b) {
+#pragma unroll
+            for (int e = 0; e < M::NACC; ++e) {
+              const int r = a * TL + M::acc_row(e, lane);
+              const int c = b * TL + M::lane_col(lane);
+              red[r * W + c] += acc[idx][e];
+            }
+            ++idx;
+          }
+      }
+    }
+    __syncthreads();
+  }
+  T* out = slabs + ((size_t)pair * nchunk + chunk) * SLAB;
+  for (int i = threadIdx.x; i < SLAB; i += kGramThreads) out[i] = red[i];
+}
+
+// -------------------------------------------------------------------- evd
+// Round-robin (circle) pairing of N indices, step st, slot a.
+__device__ __forceinline__ void rr_pair(int st, int a, int N, int& p, int& q) {
+  if (a == 0) {
+    p = st;
+    q = N - 1;
+  } else {
+    p = (st + a) % (N - 1);
+    q = (st - a + N - 1) % (N - 1);
+  }
+  if (p > q) {
+    int t = p;
+    p = q;
+    q = t;
+  }
+}
+
+// The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair:
+//   * G lives in LDS (data precision, upper triangle maintained, indexed by
+//     column id), updated per parallel step as independent 2x2 blocks
+//     (J_a^T G J_b) -- every entry belongs to exactly one block, and each
+//     thread owns a fixed set of slot-pair blocks for the whole kernel;
+//   * the rotation accumulator Q lives in REGISTERS, always in fp64, in
+//     "slot layout": lane (slot a, row group g) holds Q[k][first(a)] and
+//     Q[k][second(a)] for its rows k.  The circle-method round robin moves
+//     one player per slot to the neighbouring slot each step, which is a
+//     one-lane DPP shift (wave_shr:1 / wave_shl:1) -- no LDS traffic for Q.
+//     fp64 accumulation keeps Q orthogonal to ~1e-16 before it is rounded to
+//     the data type, so V stays orthogonal over hundreds of block steps;
+//   * per step: every lane solves its slot's rotation in the data precision
+//     (fp32 for fp32 data), one lane per slot publishes (c, s, t, p|q) as one
+//     16/32-byte record, barrier, then G blocks are updated from the records
+//     while the fp64 (c, s) for Q are formed from t off the critical path
+//     (c^2 + s^2 = 1 to fp64 accuracy), barrier, DPP shift.
+__host__ __device__ constexpr int evd_threads(int W) { return W == 64 ? 1024 : 512; }
+
+__device__ __forceinline__ int dpp_shr1(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);  // lane i <- lane i-1
+}
+__device__ __forceinline__ int dpp_shl1(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);  // lane i <- lane i+1
+}
+__device__ __forceinline__ double dpp_shr1(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = dpp_shr1((int)(x & 0xffffffff)), hi = dpp_shr1((int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double dpp_shl1(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = dpp_shl1((int)(x & 0xffffffff)), hi = dpp_shl1((int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <typename T>
+struct alignas(sizeof(T) == 8 ? 32 : 16) RotRec {
+  T c, s, t;
+  int pq;  // p | q << 16
+};
+
+template <typename T, int W>
+__global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
+    const int32_t* __restrict__ pairs, int full, const T* __restrict__ slabs, int nchunk,
+    T* __restrict__ D, T* __restrict__ Qout, int32_t* __restrict__ skip, T tol,
+    int max_inner, uint32_t* __restrict__ metric) {
+  constexpr int NT = evd_threads(W);
+  constexpr int NWAVE = NT / SVDJ_WAVE;
+  constexpr int N = 2 * W;
+  constexpr int LD = N + 1;
+  constexpr int GPW = SVDJ_WAVE / W;    // row groups per wave
+  constexpr int NGRP = NWAVE * GPW;     // row groups
+  constexpr int RPL = N / NGRP;         // Q rows per lane
+  constexpr int NBLK = W * (W + 1) / 2; // upper-triangle 2x2 blocks per step
+  constexpr int MAXB = (NBLK + NT - 1) / NT;
+  static_assert(N % NGRP == 0, "rows must split evenly over row groups");
+
+  __shared__ T G[N * LD];
+  __shared__ RotRec<T> prm[W];
+  __shared__ int sweep_rot;
+  __shared__ float wmax[NWAVE];
+
+  const int pair = blockIdx.x;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- assemble G (full symmetric storage)
+  if (full) {
+    const T* s0 = slabs + (size_t)pair * nchunk * (4 * W * W);
+    for (int i = tid; i < N * N; i += NT) {
+      T acc = 0;
+#pragma unroll 4
+      for (int c = 0; c < nchunk; ++c) acc += s0[(size_t)c * 4 * W * W + i];
+      G[(i / N) * LD + (i % N)] = acc;
+    }
+  } else {
+    const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
+    for (int i = tid; i < N * N; i += NT) G[(i / N) * LD + (i % N)] = T(0);
+    __syncthreads();
+    for (int i = tid; i < W * W; i += NT) {
+      T acc = 0;
+#pragma unroll 4
+      for (int c = 0; c < nchunk; ++c) acc += s0[(size_t)c * W * W + i];
+      const int a = i / W, b = i % W;
+      G[a * LD + W + b] = acc;
+      G[(W + b) * LD + a] = acc;
+    }
+    for (int a = tid; a < W; a += NT) {
+      G[a * LD + a] = D[bi * W + a];
+      G[(W + a) * LD + W + a] = D[bj * W + a];
+    }
+  }
+  if (tid == 0) sweep_rot = 0;
+  __syncthreads();
+
+  // ---- convergence value before any rotation
+  {
+    float mx = 0.0f;
+    for (int i = tid; i < N * N; i += NT) {
+      const int r = i / N, c = i % N;
+      const bool use = full ? (r < c) : (r < W && c >= W);
+      if (!use) continue;
+      const T d = sqrt(G[r * LD + r]) * sqrt(G[c * LD + c]);
+      if (d > T(0)) {
+        const float v = (float)(fabs(G[r * LD + c]) / d);
+        mx = v > mx ? v : mx;
+      }
+    }
+    mx = wave_max(mx);
+    if (lane == 0) wmax[wave] = mx;
+    __syncthreads();
+    if (tid == 0) {
+      float m2 = 0.0f;
+      for (int w = 0; w < NWAVE; ++w) m2 = wmax[w] > m2 ? wmax[w] : m2;
+      atomic_max_pos(&metric[0], m2);
+    }
+  }
+
+  // ---- fixed slot-pair blocks owned by this thread
+  int ba[MAXB], bb[MAXB];
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    const int idx = tid + j * NT;
+    ba[j] = bb[j] = -1;
+    if (idx < NBLK) {
+      int a = 0, base = 0;
+      while (idx >= base + (W - a)) { base += W - a; ++a; }
+      ba[j] = a;
+      bb[j] = a + (idx - base);
+    }
+  }
+
+  // ---- slot layout state
+  const int slot = lane % W;
+  const int grp = wave * GPW + lane / W;
+  int pf = slot == 0 ? N - 1 : slot;          // first player of this slot
+  int ps = slot == 0 ? 0 : N - 1 - slot;      // second player
+  double qf[RPL], qs[RPL];
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) {
+    const int k = grp * RPL + i;
+    qf[i] = (k == pf) ? 1.0 : 0.0;
+    qs[i] = (k == ps) ? 1.0 : 0.0;
+  }
+  auto sidx = [](int i, int j) { return i < j ? i * LD + j : j * LD + i; };
+
+  bool any = false;
+  for (int sw = 0; sw < max_inner; ++sw) {
+    for (int st = 0; st < N - 1; ++st) {
+      // (1) every lane solves its slot's rotation in the data precision
+      const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[sidx(pf, ps)];
+      const T nrm = sqrt(gpp) * sqrt(gqq);
+      const bool rot = nrm > T(0) && fabs(gpq) > tol * nrm;
+      T c = 1, s = 0, t = 0;
+      if (rot) schur_rotation<T>(gpq, gpp, gqq, c, s, t);
+      if (wave == 0 && lane < W) {
+        RotRec<T> r;
+        r.c = c;
+        r.s = s;
+        r.t = t;
+        r.pq = pf | (ps << 16);
+        prm[slot] = r;
+        if (rot) sweep_rot = 1;
+      }
+      __syncthreads();
+      // (2) G <- J^T G J on this thread's upper-triangle 2x2 blocks
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) {
+        if (ba[j] < 0) continue;
+        const RotRec<T> A = prm[ba[j]];
+        const int p = A.pq & 0xffff, q = A.pq >> 16;
+        if (ba[j] == bb[j]) {
+          if (A.s != T(0)) {
+            const int ipq = sidx(p, q);
+            const T v = G[ipq];
+            G[p * LD + p] -= A.t * v;
+            G[q * LD + q] += A.t * v;
+            G[ipq] = T(0);
+          }
+        } else {
+          const RotRec<T> B = prm[bb[j]];
+          const int r = B.pq & 0xffff, u = B.pq >> 16;
+          const int i00 = sidx(p, r), i01 = sidx(p, u), i10 = sidx(q, r), i11 = sidx(q, u);
+          const T g00 = G[i00], g01 = G[i01], g10 = G[i10], g11 = G[i11];
+          const T h00 = A.c * g00 - A.s * g10, h01 = A.c * g01 - A.s * g11;
+          const T h10 = A.s * g00 + A.c * g10, h11 = A.s * g01 + A.c * g11;
+          G[i00] = B.c * h00 - B.s * h01;
+          G[i01] = B.s * h00 + B.c * h01;
+          G[i10] = B.c * h10 - B.s * h11;
+          G[i11] = B.s * h10 + B.c * h11;
+        }
+      }
+      // (3) Q <- Q J in registers (fp64 rotation, normalised from t)
+      if (rot) {
+        double c64, s64;
+        if constexpr (sizeof(T) == 8) {
+          c64 = c;
+          s64 = s;
+        } else {
+          const double td = (double)t;
+          c64 = 1.0 / sqrt(1.0 + td * td);
+          s64 = td * c64;
+        }
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+          const double x = qf[i], y = qs[i];
+          qf[i] = c64 * x - s64 * y;
+          qs[i] = s64 * x + c64 * y;
+        }
+      }
+      __syncthreads();
+      // (4) advance the round robin: firsts shift right, seconds shift left
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) {
+        const double f_r = dpp_shr1(qf[i]), s_r = dpp_shr1(qs[i]), s_l = dpp_shl1(qs[i]);
+        const double nf = slot == 0 ? qf[i] : (slot == 1 ? s_r : f_r);
+        const double ns = slot == W - 1 ? qf[i] : s_l;
+        qf[i] = nf;
+        qs[i] = ns;
+      }
+      {
+        const int f_r = dpp_shr1(pf), s_r = dpp_shr1(ps), s_l = dpp_shl1(ps);
+        const int nf = slot == 0 ? pf : (slot == 1 ? s_r : f_r);
+        const int ns = slot == W - 1 ? pf : s_l;
+        pf = nf;
+        ps = ns;
+      }
+    }
+    const int rot = sweep_rot;
+    __syncthreads();
+    if (tid == 0) sweep_rot = 0;
+    if (!rot) break;
+    any = true;
+    __syncthreads();
+  }
+
+  if (tid == 0) {
+    skip[pair] = any ? 0 : 1;
+    if (any) atomicAdd(&metric[1], 1u);
+  }
+  // Full mode re-measured the diagonal from the data: always refresh D.
+  if (!any && !full) return;
+  if (any) {
+    T* qo = Qout + (size_t)pair * N * N;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int k = grp * RPL + i;
+      qo[k * N + pf] = (T)qf[i];
+      qo[k * N + ps] = (T)qs[i];
+    }
+  }
+  for (int a = tid; a < N; a += NT) {
+    const int col = (a < W ? bi * W + a : bj * W + (a - W));
+    D[col] = G[a * LD + a];
+  }
+}
+
+// ------------------------------------------------------------------ apply
+template <typename T, int W>
+__global__ __launch_bounds__(kApplyThreads) void apply_kernel(
+    T* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, T* __restrict__ V,
+    int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs, const T* __restrict__ Qall,
+    const int32_t* __restrict__ skip) {
+  using M = Mfma<T>;
+  constexpr int TL = M::TILE;
+  constexpr int KG = M::KG;
+  constexpr int N = 2 * W;
+  constexpr int NK = N / KG;   // k values per lane
+  constexpr int NCT = N / TL;  // output column tiles
+  constexpr int LDQ = N + (sizeof(T) == 8 ? 16 : 0);
+  constexpr int WAVES = kApplyThreads / SVDJ_WAVE;
+  __shared__ T Qs[N * LDQ];
+
+  const int pair = blockIdx.x;
+  if (skip[pair]) return;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  int chunk = blockIdx.y;
+  T* base;
+  int ld, r_begin, r_end;
+  if (chunk < a_chunks) {
+    base = A;
+    ld = lda;
+    r_begin = chunk * rows_a;
+    r_end = min(m_pad, r_begin + rows_a);
+  } else {
+    chunk -= a_chunks;
+    base = V;
+    ld = ldv;
+    r_begin = chunk * rows_v;
+    r_end = min(n_v, r_begin + rows_v);
+  }
+  const T* Qg = Qall + (size_t)pair * N * N;
+  for (int i = threadIdx.x; i < N * N; i += kApplyThreads) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lc = M::lane_col(lane), kg = M::lane_kg(lane);
+  // Column k of X = [A_bi A_bj] is base + col(k)*ld.  The lane-dependent
+  // part of every address (k group, row lane, acc row group) is folded into
+  // one 64-bit lane offset; the per-k / per-tile part is wave-uniform, so the
+  // address arithmetic stays in SGPRs.
+  T* const xi = base + (size_t)bi * W * ld;
+  T* const xj = base + (size_t)bj * W * ld;
+  const uint32_t ld_off = (uint32_t)(kg * ld + lc);
+  const uint32_t st_off = (uint32_t)(M::acc_row_lane(lane) * ld + lc);
+  // Q fragments are loop-invariant: small Q (<= 64 VGPRs of fragments) is
+  // left to the compiler to hoist into registers; larger Q is re-read from
+  // LDS per row tile (the empty asm with a memory clobber blocks the hoist).
+  constexpr bool kHoistQ = (NK * NCT * (int)sizeof(T)) / 4 <= 64;
+  auto load_tile = [&](T (&x)[NK], int r) {
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const int k0 = kk * KG;
+      const T* src = (k0 < W ? xi + (size_t)k0 * ld : xj + (size_t)(k0 - W) * ld);
+      x[kk] = src[ld_off + (uint32_t)r];
+    }
+  };
+  int r0 = r_begin + wave * TL;
+  if (r0 >= r_end) return;
+  T xv[NK];
+  load_tile(xv, r0);
+  while (true) {
+    const int rn = r0 + WAVES * TL;
+    const bool more = rn < r_end;
+    T xn[NK];
+    if (more) load_tile(xn, rn);  // next tile in flight during this tile's MFMAs
+    if constexpr (!kHoistQ) asm volatile("" ::: "memory");
+    constexpr int kCtUnroll = kHoistQ ? NCT : 1;
+#pragma unroll kCtUnroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      typename M::acc_t acc = M::zero();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const T a = Qs[(kk * KG + kg) * LDQ + ct * TL + lc];
+        acc = M::mfma(a, xv[kk], acc);
+      }
+      const int c0 = ct * TL;
+      T* dst = (c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld);
+#pragma unroll
+      for (int e = 0; e < M::NACC; ++e)
+        dst[(size_t)M::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = acc[e];
+    }
+    if (!more) break;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) xv[kk] = xn[kk];
+    r0 = rn;
+  }
+}
+
+// ------------------------------------------------------------- host side
+struct Geometry {
+  int gchunks, grows;  // gram
+  int a_chunks, rows_a, v_chunks, rows_v;
+};
+
+static Geometry make_geometry(int P, int m_pad, int n_v) {
+  Geometry g;
+  // Gram: aim for >= 2 waves of workgroups over 256 CUs, >= 128 rows/chunk.
+  int want = (512 + P - 1) / P;
+  int maxc = m_pad / 128;
+  g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
+  g.grows = round_up((m_pad + g.gchunks - 1) / g.gchunks, 128);
+  g.gchunks = (m_pad + g.grows - 1) / g.grows;
+  // Apply: ~1024+ workgroups over A and V rows, >= 128 rows each.
+  int total_rows = m_pad + n_v;
+  int wg_target = 2048;
+  int rows = round_up((int)(((long)total_rows * P + wg_target - 1) / wg_target), 128);
+  if (rows < 128) rows = 128;
+  if (rows > 2048) rows = 2048;
+  g.rows_a = rows;
+  g.rows_v = rows;
+  g.a_chunks = (m_pad + rows - 1) / rows;
+  g.v_chunks = n_v > 0 ? (n_v + rows - 1) / rows : 0;
+  return g;
+}
+
+static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
+  Geometry g = make_geometry(P, m_pad, 0);
+  size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
+  size_t q = (size_t)P * 4 * W * W * esize;
+  size_t sk = (size_t)P * sizeof(int32_t);
+  return ((slabs + 255) / 256 * 256) + ((q + 255) / 256 * 256) + ((sk + 255) / 256 * 256);
+}
+
+template <typename T, int W>
+static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
+                         const int32_t* pairs, int P, int steps, const int32_t* modes,
+                         double tol, int max_inner, void* ws, size_t ws_bytes,
+                         uint32_t* metric, hipStream_t st) {
+  const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad);
+  if (ws_bytes < need) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, need);
+    return -4;
+  }
+  Geometry g = make_geometry(P, m_pad, V ? n_v : 0);
+  char* w = (char*)ws;
+  T* slabs = (T*)w;
+  w += ((size_t)P * g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
+  T* Q = (T*)w;
+  w += ((size_t)P * 4 * W * W * sizeof(T) + 255) / 256 * 256;
+  int32_t* skip = (int32_t*)w;
+  for (int s = 0; s < steps; ++s) {
+    const int32_t* pr = pairs + (size_t)s * P * 2;
+    const int full = modes ? modes[s] : 0;
+    if (full)
+      hipLaunchKernelGGL((gram_kernel<T, W, true>), dim3(P, g.gchunks), dim3(kGramThreads), 0, st,
+                         A, lda, m_pad, pr, g.grows, slabs);
+    else
+      hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(P, g.gchunks), dim3(kGramThreads), 0,
+                         st, A, lda, m_pad, pr, g.grows, slabs);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full, slabs,
+                       g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks + g.v_chunks),
+                       dim3(kApplyThreads), 0, st, A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv,
+                       g.rows_v, V ? n_v : 0, pr, Q, skip);
+    SVDJ_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace svdj
+
+using namespace svdj;
+
+extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
+  return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);
+}
+
+extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                int ldv, void* D, const int32_t* pairs, int P, int steps,
+                                const int32_t* modes, double tol, int max_inner, void* ws,
+                                size_t ws_bytes, uint32_t* metric, void* stream) {
+  if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad) {
+    set_error("bad m_pad/lda %d/%d", m_pad, lda);
+    return -2;
+  }
+  if (V && (n_v <= 0 || n_v % SVDJ_ROW_ALIGN || ldv < n_v)) {
+    set_error("bad n_v/ldv %d/%d", n_v, ldv);
+    return -2;
+  }
+  if (P <= 0 || steps < 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 0 && W == 32)
+    return block_steps_t<float, 32>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
+                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, st);
+  if (dtype == 0 && W == 64)
+    return block_steps_t<float, 64>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
+                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, st);
+  if (dtype == 1 && W == 32)
+    return block_steps_t<double, 32>(m_pad, (double*)A, lda, (double*)V, n_v, ldv, (double*)D,
+                                     pairs, P, steps, modes, tol, max_inner, ws, ws_bytes,
+                                     metric, st);
+  set_error("unsupported (dtype=%d, W=%d); supported: fp32 W in {32,64}, fp64 W=32", dtype, W);
+  return -3;
+}
+
+extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                int ldv, void* D, int ncols, double tol, int max_inner,
+                                int max_sweeps, void* ws, size_t ws_bytes, uint32_t* metric,
+                                double* hist, int use_graph, void* stream) {
+  (void)use_graph;
+  if (W <= 0 || ncols % W) {
+    set_error("ncols %d not a multiple of W %d", ncols, W);
+    return -2;
+  }
+  const int nb = ncols / W;
+  if (nb < 2 || (nb & 1)) {
+    set_error("block count %d must be even and >= 2", nb);
+    return -2;
+  }
+  const int P = nb / 2, steps = nb - 1;
+  std::vector<int32_t> h((size_t)steps * P * 2);
+  for (int r = 0; r < steps; ++r) {
+    int32_t* o = h.data() + (size_t)r * P * 2;
+    o[0] = r;
+    o[1] = nb - 1;
+    for (int k = 1; k < P; ++k) {
+      int a = (r + k) % (nb - 1), b = (r - k + nb - 1) % (nb - 1);
+      o[2 * k] = a < b ? a : b;
+      o[2 * k + 1] = a < b ? b : a;
+    }
+  }
+  std::vector<int32_t> modes(steps, 0);
+  modes[0] = 1;
+  hipStream_t st = (hipStream_t)stream;
+  int32_t* dpairs = nullptr;
+  SVDJ_HIP_CHECK(hipMallocAsync((void**)&dpairs, h.size() * sizeof(int32_t), st));
+  SVDJ_HIP_CHECK(hipMemcpyAsync(dpairs, h.data(), h.size() * sizeof(int32_t),
+                                hipMemcpyHostToDevice, st));
+  int sweeps = 0, rc = 0;
+  uint32_t hm[2];
+  for (int sw = 0; sw < max_sweeps; ++sw) {
+    if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
+    rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,
+                          modes.data(), tol, max_inner, ws, ws_bytes, metric, stream);
+    if (rc) break;
+    if (hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      set_error("metric readback failed");
+      rc = -100;
+      break;
+    }
+    float mx;
+    memcpy(&mx, &hm[0], sizeof(float));
+    if (hist) hist[sw] = mx;
+    sweeps = sw + 1;
+    if (hm[1] == 0) break;
+  }
+  (void)hipFreeAsync(dpairs, st);
+  return rc ? rc : sweeps;
+}

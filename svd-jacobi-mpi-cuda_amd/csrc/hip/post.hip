@@ -1,0 +1,137 @@
+// Initialisation / post-processing kernels and library utilities.
+//
+// Replaces the reference's OpenMP host loops for V := I
+// (reference main.cu:461-474) and for sigma / U (main.cu:1394-1421):
+//   * sigma_k = ||a_k|| with fp64 accumulation (one wave per column),
+//   * U = A / sigma with a sigma == 0 guard (the reference divides blindly),
+//   * squared column norms D used to seed the block path.
+#include "common.hpp"
+#include "svdj_hip.h"
+
+#include <stdarg.h>
+#include <string.h>
+
+namespace svdj {
+
+static thread_local char g_err[512] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void identity_kernel(T* V, int n_v, int ldv, int ncols,
+                                                        int col_offset) {
+  const int c = blockIdx.x;
+  T* col = V + (size_t)c * ldv;
+  const int diag = c + col_offset;
+  for (int i = threadIdx.x; i < n_v; i += blockDim.x) col[i] = (i == diag) ? T(1) : T(0);
+}
+
+// One wave per column: sum of squares in fp64.
+template <typename T>
+__global__ __launch_bounds__(256) void colnorm2_kernel(const T* __restrict__ A, int m_pad,
+                                                        int lda, int ncols, T* __restrict__ D) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + wave;
+  if (c >= ncols) return;
+  const T* a = A + (size_t)c * lda;
+  double acc = 0.0;
+  for (int i = lane; i < m_pad; i += 64) {
+    const double x = (double)a[i];
+    acc += x * x;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) D[c] = (T)acc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void finalize_kernel(T* __restrict__ A, int m_pad, int lda,
+                                                        int ncols, T* __restrict__ sigma,
+                                                        int scale_u) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + wave;
+  if (c >= ncols) return;
+  T* a = A + (size_t)c * lda;
+  double acc = 0.0;
+  for (int i = lane; i < m_pad; i += 64) {
+    const double x = (double)a[i];
+    acc += x * x;
+  }
+  acc = wave_sum(acc);
+  const double nrm = sqrt(acc);
+  if (lane == 0) sigma[c] = (T)nrm;
+  if (scale_u && nrm > 0.0) {
+    const T inv = (T)(1.0 / nrm);
+    for (int i = lane; i < m_pad; i += 64) a[i] *= inv;
+  }
+}
+
+}  // namespace svdj
+
+using namespace svdj;
+
+extern "C" const char* svdj_hip_last_error(void) { return g_err; }
+
+extern "C" const char* svdj_hip_version(void) {
+  return "svdj-hip 0.1 gfx950 (mfma_f32_32x32x2f32, mfma_f64_16x16x4f64)";
+}
+
+extern "C" int svdj_set_identity(int dtype, void* V, int n_v, int ldv, int ncols, int col_offset,
+                                 void* stream) {
+  if (ncols <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(identity_kernel<float>, dim3(ncols), dim3(256), 0, st, (float*)V, n_v, ldv,
+                       ncols, col_offset);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(identity_kernel<double>, dim3(ncols), dim3(256), 0, st, (double*)V, n_v,
+                       ldv, ncols, col_offset);
+  else {
+    set_error("unsupported dtype %d", dtype);
+    return -3;
+  }
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int ncols, void* D,
+                               void* stream) {
+  if (ncols <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (ncols + 3) / 4;
+  if (dtype == 0)
+    hipLaunchKernelGGL(colnorm2_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)A,
+                       m_pad, lda, ncols, (float*)D);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(colnorm2_kernel<double>, dim3(blocks), dim3(256), 0, st, (const double*)A,
+                       m_pad, lda, ncols, (double*)D);
+  else {
+    set_error("unsupported dtype %d", dtype);
+    return -3;
+  }
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma,
+                             int scale_u, void* stream) {
+  if (ncols <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (ncols + 3) / 4;
+  if (dtype == 0)
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3(blocks), dim3(256), 0, st, (float*)A, m_pad,
+                       lda, ncols, (float*)sigma, scale_u);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(finalize_kernel<double>, dim3(blocks), dim3(256), 0, st, (double*)A, m_pad,
+                       lda, ncols, (double*)sigma, scale_u);
+  else {
+    set_error("unsupported dtype %d", dtype);
+    return -3;
+  }
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}

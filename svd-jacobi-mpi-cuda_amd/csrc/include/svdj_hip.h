@@ -1,0 +1,90 @@
+// Device-side (MI355X / gfx950) native API of the Jacobi-SVD framework.
+//
+// Plain C ABI over raw device pointers + a hipStream_t passed as void*, so the
+// library has no PyTorch dependency: Python binds it with ctypes and passes
+// tensor.data_ptr() / torch.cuda.current_stream().cuda_stream; the native C++
+// driver links it directly.
+//
+// Storage convention (all entry points): a column-major matrix with leading
+// dimension ld is addressed as column c at base + c*ld.  Row counts passed to
+// kernels are PADDED row counts (multiple of SVDJ_ROW_ALIGN, pad rows zero),
+// so no kernel needs a row bounds check.
+//
+// dtype codes: 0 = fp32, 1 = fp64.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#define SVDJ_ROW_ALIGN 128
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Returns a static version/feature string ("gfx950 ...").
+const char* svdj_hip_version(void);
+// Last error message recorded by this library (thread-local), "" if none.
+const char* svdj_hip_last_error(void);
+
+// ---------------------------------------------------------------------------
+// Scalar (column-pair) path: one fused kernel per parallel step, one
+// workgroup per pair (wave64 reductions of the reference's dot triple,
+// rotation solved in registers, Givens update of A and V in place).
+//   sched     device int32 [steps][per_step][2] (pairs < 0 are skipped)
+//   tol_mode  0 relative, 1 absolute
+//   metric    device uint32[2]: [0] = max convergence value (float bits),
+//             [1] = number of rotations applied.  Accumulated (not reset).
+int svdj_scalar_step(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
+                     int ldv, const int32_t* sched, int per_step, double tol,
+                     int tol_mode, uint32_t* metric, void* stream);
+
+// Full solve on one GPU: repeats sweeps over `steps` until a sweep applies
+// no rotation or max_sweeps is reached.  hist (host, may be NULL) receives
+// the per-sweep max convergence value.  Returns sweeps executed, <0 on error.
+int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
+                      int ldv, const int32_t* sched, int steps, int per_step,
+                      double tol, int tol_mode, int max_sweeps, uint32_t* metric,
+                      double* hist, void* stream);
+
+// ---------------------------------------------------------------------------
+// Block path (one-sided block Jacobi, MFMA).  Columns are grouped in blocks
+// of W (32 or 64; fp64 supports 32).  One step processes P disjoint block
+// pairs (bi, bj):
+//   1. Gram (MFMA, split over rows):  mode 0 (cross) C = A_bi^T A_bj,
+//                                     mode 1 (full)  G = [A_bi A_bj]^T[..]
+//   2. EVD of the 2W x 2W Gram (cyclic parallel Jacobi in LDS), in cross
+//      mode with the diagonal blocks taken from the tracked squared column
+//      norms D (blocks are kept internally orthogonal);  Q -> workspace.
+//   3. Apply (MFMA):  [A_bi A_bj] <- [A_bi A_bj] Q ,  [V_bi V_bj] <- .. Q
+// D (device, dtype, [ncols]) holds squared column norms; updated in place.
+//   pairs   device int32 [steps][P][2] block indices
+//   modes   host   int32 [steps] (0 cross / 1 full), NULL = all cross
+//   metric  device uint32[2] as for the scalar path.
+// Workspace size for one step: svdj_block_workspace_bytes().
+size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
+int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
+                     int n_v, int ldv, void* D, const int32_t* pairs, int P,
+                     int steps, const int32_t* modes, double tol,
+                     int max_inner_sweeps, void* workspace, size_t ws_bytes,
+                     uint32_t* metric, void* stream);
+
+// Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
+// first step of every sweep in full mode.  Returns sweeps, <0 on error.
+int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
+                     int n_v, int ldv, void* D, int ncols, double tol,
+                     int max_inner_sweeps, int max_sweeps, void* workspace,
+                     size_t ws_bytes, uint32_t* metric, double* hist,
+                     int use_graph, void* stream);
+
+// ---------------------------------------------------------------------------
+// Post-processing / utilities.
+// V := I on an (n_v x ncols) column-major block (rows >= ncols zeroed).
+int svdj_set_identity(int dtype, void* V, int n_v, int ldv, int ncols, int col_offset, void* stream);
+// Squared column norms D[c] = sum_i A[i,c]^2 (fp64 accumulation).
+int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int ncols, void* D, void* stream);
+// sigma[c] = ||a_c||; if scale_u, a_c /= sigma[c] (sigma == 0 columns untouched).
+int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma, int scale_u, void* stream);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,133 @@
+"""ctypes bindings of the two in-tree native libraries.
+
+``libsvdj_cpu.so`` (host C++) is always required.  ``libsvdj_hip.so`` (gfx950
+kernels) is required for any CUDA/HIP tensor: if it is missing or fails to
+load on a GPU box the call raises -- there is no silent PyTorch fallback for
+device tensors.  CPU tensors use the torch reference implementations in
+``ops/reference.py`` (the oracle path used by CPU tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent.parent
+_LIBDIR = _PKG / "lib"
+_lock = threading.Lock()
+_cpu = None
+_hip = None
+
+c_int = C.c_int
+c_double = C.c_double
+c_size_t = C.c_size_t
+c_void_p = C.c_void_p
+c_u32_p = C.POINTER(C.c_uint32)
+c_i32_p = C.POINTER(C.c_int32)
+c_f64_p = C.POINTER(C.c_double)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _ensure_built(which: str) -> Path:
+    from .. import _build
+
+    path = _build.CPU_LIB if which == "cpu" else _build.HIP_LIB
+    if os.environ.get("SVDJ_NO_AUTOBUILD") == "1":
+        if not path.exists():
+            raise NativeError(f"{path} missing and SVDJ_NO_AUTOBUILD=1")
+        return path
+    if which == "cpu":
+        return _build.build_cpu()
+    return _build.build_hip()
+
+
+def _sig(lib, name, restype, argtypes):
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = argtypes
+    return fn
+
+
+def cpu_lib():
+    """Host library (schedules, oracle, RNG, verification)."""
+    global _cpu
+    if _cpu is not None:
+        return _cpu
+    with _lock:
+        if _cpu is not None:
+            return _cpu
+        lib = C.CDLL(str(_ensure_built("cpu")))
+        _sig(lib, "svdj_sameh_num_steps", c_int, [c_int])
+        _sig(lib, "svdj_sameh_schedule", c_int, [c_int, c_i32_p])
+        _sig(lib, "svdj_round_robin", c_int, [c_int, c_i32_p])
+        _sig(lib, "svdj_bipartite", c_int, [c_int, c_i32_p])
+        _sig(lib, "svdj_tournament", c_int, [c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
+        for name, ptr in (("svdj_cpu_jacobi_f64", C.POINTER(C.c_double)),
+                          ("svdj_cpu_jacobi_f32", C.POINTER(C.c_float))):
+            _sig(lib, name, c_int, [c_int, c_int, c_int, c_int, ptr, c_int, ptr, ptr, c_int,
+                                    c_int, c_int, c_double, c_int, c_f64_p, c_int])
+        _sig(lib, "svdj_ref_triu_input", None, [c_int, c_int, c_f64_p, c_int, C.c_uint32])
+        _sig(lib, "svdj_ref_dense_input", None, [c_int, c_int, c_f64_p, c_int, C.c_uint32])
+        _sig(lib, "svdj_ref_uniform_stream", None, [C.c_uint32, c_int, c_f64_p])
+        _sig(lib, "svdj_cpu_residual_f64", c_double,
+             [c_int, c_int, c_int, c_f64_p, c_int, c_f64_p, c_int, c_f64_p, c_f64_p, c_int, c_int])
+        _sig(lib, "svdj_cpu_orth_f64", c_double, [c_int, c_int, c_f64_p, c_int, c_int])
+        _sig(lib, "svdj_cpu_version", C.c_char_p, [])
+        _cpu = lib
+        return lib
+
+
+def hip_lib():
+    """gfx950 kernel library.  Raises NativeError if unavailable."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    with _lock:
+        if _hip is not None:
+            return _hip
+        import torch  # noqa: F401  -- load torch's HIP runtime first (shared soname)
+
+        path = _ensure_built("hip")
+        try:
+            lib = C.CDLL(str(path))
+        except OSError as e:  # pragma: no cover - GPU box only
+            raise NativeError(f"cannot load {path}: {e}") from e
+        _sig(lib, "svdj_hip_version", C.c_char_p, [])
+        _sig(lib, "svdj_hip_last_error", C.c_char_p, [])
+        _sig(lib, "svdj_scalar_step", c_int,
+             [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_double,
+              c_int, c_void_p, c_void_p])
+        _sig(lib, "svdj_scalar_solve", c_int,
+             [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+              c_double, c_int, c_int, c_void_p, c_f64_p, c_void_p])
+        _sig(lib, "svdj_block_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int])
+        _sig(lib, "svdj_block_steps", c_int,
+             [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+              c_int, c_int, c_i32_p, c_double, c_int, c_void_p, c_size_t, c_void_p, c_void_p])
+        _sig(lib, "svdj_block_solve", c_int,
+             [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
+              c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int, c_void_p])
+        _sig(lib, "svdj_set_identity", c_int,
+             [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
+        _sig(lib, "svdj_col_norms2", c_int, [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p])
+        _sig(lib, "svdj_finalize", c_int,
+             [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p])
+        _hip = lib
+        return lib
+
+
+def hip_check(rc: int, what: str) -> int:
+    if rc < 0:
+        msg = hip_lib().svdj_hip_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (rc={rc}): {msg}")
+    return rc
+
+
+def loaded_libraries() -> dict:
+    """Which native libraries this process has loaded (for reports/tests)."""
+    return {"cpu": _cpu is not None, "hip": _hip is not None,
+            "cpu_path": str(_LIBDIR / "libsvdj_cpu.so"), "hip_path": str(_LIBDIR / "libsvdj_hip.so")}

@@ -1,0 +1,244 @@
+"""Tensor-level entry points of the native ops.
+
+Device (HIP) tensors go to the gfx950 kernels in ``libsvdj_hip.so`` via
+ctypes on torch's current stream; CPU tensors go to ``ops.reference``.  A
+device tensor never falls back to PyTorch math: a missing/failed native
+library raises :class:`NativeError`.
+
+All matrices use the transposed column-major layout of the kernels: ``At``
+has shape (ncols, ld) and row c is column c of the matrix; rows are padded to
+``ROW_ALIGN`` with zeros (``m_pad``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+
+import numpy as np
+import torch
+
+from . import reference as ref
+from ._native import NativeError, hip_check, hip_lib
+
+ROW_ALIGN = 128
+SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32,)}
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.float32:
+        return 0
+    if dtype == torch.float64:
+        return 1
+    raise TypeError(f"unsupported dtype {dtype} (fp32/fp64)")
+
+
+def _stream(t: torch.Tensor):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _check_layout(At: torch.Tensor, m_pad: int):
+    if At.dim() != 2 or At.stride(1) != 1:
+        raise ValueError("At must be a 2-D tensor with contiguous rows (ncols, ld)")
+    if m_pad % ROW_ALIGN or At.stride(0) < m_pad or At.shape[1] < m_pad:
+        raise ValueError(f"m_pad={m_pad} must be a multiple of {ROW_ALIGN} and <= ld")
+
+
+# ------------------------------------------------------------------ metric
+def new_metric(device) -> torch.Tensor:
+    if torch.device(device).type == "cpu":
+        return torch.zeros(2, dtype=torch.float64)
+    return torch.zeros(2, dtype=torch.int32, device=device)
+
+
+def reset_metric(metric: torch.Tensor):
+    metric.zero_()
+
+
+def read_metric(metric: torch.Tensor):
+    """(max convergence value, rotations) -- synchronises for device metrics."""
+    if metric.device.type == "cpu":
+        return float(metric[0]), int(metric[1])
+    h = metric.cpu().numpy().astype(np.int32)
+    mx = struct.unpack("<f", struct.pack("<i", int(h[0])))[0]
+    return mx, int(np.uint32(h[1]))
+
+
+def metric_as_float_pair(metric: torch.Tensor) -> torch.Tensor:
+    """Device-side (maxconv, rotations) as float64 without host sync."""
+    if metric.device.type == "cpu":
+        return metric.clone()
+    return torch.stack([metric[0:1].view(torch.float32).double()[0], metric[1].double()])
+
+
+# --------------------------------------------------------------- utilities
+def set_identity(Vt: torch.Tensor, ncols: int, col_offset: int = 0):
+    if Vt.is_cuda:
+        hip_check(hip_lib().svdj_set_identity(dtype_code(Vt.dtype), _ptr(Vt), Vt.shape[1],
+                                              Vt.stride(0), ncols, col_offset, _stream(Vt)),
+                  "set_identity")
+    else:
+        Vt[:ncols].zero_()
+        idx = torch.arange(ncols)
+        ok = idx + col_offset < Vt.shape[1]
+        Vt[idx[ok], idx[ok] + col_offset] = 1
+
+
+def col_norms2(At: torch.Tensor, m_pad: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    _check_layout(At, m_pad)
+    ncols = At.shape[0]
+    if out is None:
+        out = torch.empty(ncols, dtype=At.dtype, device=At.device)
+    if At.is_cuda:
+        hip_check(hip_lib().svdj_col_norms2(dtype_code(At.dtype), _ptr(At), m_pad, At.stride(0),
+                                            ncols, _ptr(out), _stream(At)), "col_norms2")
+    else:
+        out.copy_(ref.col_norms2(At[:, :m_pad]))
+    return out
+
+
+def finalize(At: torch.Tensor, m_pad: int, scale_u: bool = True) -> torch.Tensor:
+    """sigma_c = ||a_c||; optionally a_c /= sigma_c (sigma 0 untouched)."""
+    _check_layout(At, m_pad)
+    ncols = At.shape[0]
+    sigma = torch.empty(ncols, dtype=At.dtype, device=At.device)
+    if At.is_cuda:
+        hip_check(hip_lib().svdj_finalize(dtype_code(At.dtype), _ptr(At), m_pad, At.stride(0),
+                                          ncols, _ptr(sigma), int(scale_u), _stream(At)),
+                  "finalize")
+    else:
+        sigma.copy_(ref.finalize(At[:, :m_pad], scale_u))
+    return sigma
+
+
+# ---------------------------------------------------------------- scalar path
+def scalar_step(At, Vt, m_pad, pairs, tol, tol_mode, metric):
+    """One parallel step; pairs: int32 tensor (k, 2) on At's device."""
+    _check_layout(At, m_pad)
+    if At.is_cuda:
+        n_v = Vt.shape[1] if Vt is not None else 0
+        ldv = Vt.stride(0) if Vt is not None else 0
+        hip_check(hip_lib().svdj_scalar_step(
+            dtype_code(At.dtype), m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
+            _ptr(pairs), pairs.shape[0], float(tol), int(tol_mode), _ptr(metric), _stream(At)),
+            "scalar_step")
+    else:
+        mx, nrot = ref.scalar_step(At, Vt, pairs, tol, tol_mode)
+        metric[0] = max(float(metric[0]), mx)
+        metric[1] += nrot
+
+
+def scalar_solve(At, Vt, m_pad, sched, tol, tol_mode, max_sweeps):
+    """Repeated sweeps over ``sched`` (int32 (steps, per_step, 2)) until no
+    rotation.  Returns (sweeps, per-sweep max convergence value list)."""
+    _check_layout(At, m_pad)
+    steps, per_step = int(sched.shape[0]), int(sched.shape[1])
+    if At.is_cuda:
+        metric = new_metric(At.device)
+        hist = (C.c_double * max(max_sweeps, 1))()
+        n_v = Vt.shape[1] if Vt is not None else 0
+        ldv = Vt.stride(0) if Vt is not None else 0
+        sweeps = hip_check(hip_lib().svdj_scalar_solve(
+            dtype_code(At.dtype), m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
+            _ptr(sched), steps, per_step, float(tol), int(tol_mode), int(max_sweeps),
+            _ptr(metric), hist, _stream(At)), "scalar_solve")
+        return sweeps, [hist[i] for i in range(sweeps)]
+    hist = []
+    for _ in range(max_sweeps):
+        metric = new_metric("cpu")
+        for s in range(steps):
+            scalar_step(At, Vt, m_pad, sched[s], tol, tol_mode, metric)
+        mx, nrot = read_metric(metric)
+        hist.append(mx)
+        if nrot == 0:
+            break
+    return len(hist), hist
+
+
+# ----------------------------------------------------------------- block path
+_WS_CACHE: dict = {}
+
+
+def block_workspace(dtype, W, P, m_pad, device) -> torch.Tensor:
+    nbytes = int(hip_lib().svdj_block_workspace_bytes(dtype_code(dtype), W, P, m_pad))
+    key = (torch.device(device), dtype, W, P, m_pad)
+    ws = _WS_CACHE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS_CACHE[key] = ws
+    return ws
+
+
+def check_block(dtype, W):
+    if W not in SUPPORTED_BLOCK.get(dtype, ()):
+        raise ValueError(f"block width {W} unsupported for {dtype}; supported "
+                         f"{SUPPORTED_BLOCK.get(dtype, ())}")
+
+
+def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric):
+    """Run ``len(modes)`` block steps.  pairs: int32 (steps, P, 2) on At's
+    device (block indices local to At); modes: list of 0 (cross) / 1 (full)."""
+    _check_layout(At, m_pad)
+    check_block(At.dtype, W)
+    steps, P = int(pairs.shape[0]), int(pairs.shape[1])
+    if steps == 0 or P == 0:
+        return
+    if At.is_cuda:
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device)
+        md = (C.c_int32 * steps)(*[int(x) for x in modes])
+        n_v = Vt.shape[1] if Vt is not None else 0
+        ldv = Vt.stride(0) if Vt is not None else 0
+        hip_check(hip_lib().svdj_block_steps(
+            dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
+            _ptr(D), _ptr(pairs), P, steps, md, float(tol), int(max_inner), _ptr(ws),
+            ws.numel(), _ptr(metric), _stream(At)), "block_steps")
+    else:
+        for s in range(steps):
+            mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, bool(modes[s]), tol,
+                                      max_inner)
+            metric[0] = max(float(metric[0]), mx)
+            metric[1] += nrot
+
+
+def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, use_graph=False):
+    """Single-device block Jacobi (round-robin over ncols/W blocks, first
+    step of each sweep full).  Returns (sweeps, hist)."""
+    _check_layout(At, m_pad)
+    check_block(At.dtype, W)
+    ncols = At.shape[0]
+    if At.is_cuda:
+        nb = ncols // W
+        ws = block_workspace(At.dtype, W, nb // 2, m_pad, At.device)
+        metric = new_metric(At.device)
+        hist = (C.c_double * max(max_sweeps, 1))()
+        n_v = Vt.shape[1] if Vt is not None else 0
+        ldv = Vt.stride(0) if Vt is not None else 0
+        sweeps = hip_check(hip_lib().svdj_block_solve(
+            dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
+            ncols, float(tol), int(max_inner), int(max_sweeps), _ptr(ws), ws.numel(),
+            _ptr(metric), hist, int(use_graph), _stream(At)), "block_solve")
+        return sweeps, [hist[i] for i in range(sweeps)]
+    from ..parallel.schedule import round_robin
+
+    nb = ncols // W
+    pairs = torch.from_numpy(round_robin(nb))
+    modes = [1] + [0] * (nb - 2)
+    hist = []
+    for _ in range(max_sweeps):
+        metric = new_metric("cpu")
+        block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric)
+        mx, nrot = read_metric(metric)
+        hist.append(mx)
+        if nrot == 0:
+            break
+    return len(hist), hist
+
+
+__all__ = [
+    "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "dtype_code", "new_metric", "reset_metric",
+    "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
+    "block_workspace", "block_steps", "block_solve", "check_block",
+]

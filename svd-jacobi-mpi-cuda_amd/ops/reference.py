@@ -1,0 +1,187 @@
+"""Plain-PyTorch reference implementations of every device op.
+
+These run on CPU tensors.  They are the numerics oracle for the HIP kernels
+(tests compare kernel output against them, in fp64) and the compute path of
+the CPU-only multi-process tests (gloo), so the distributed orchestration is
+exercised end to end without a GPU.  They are never used for GPU tensors.
+
+Layout: a column-major matrix is held as its transpose ``At`` (ncols, ld):
+row c of ``At`` is column c of the matrix (contiguous, like the kernels).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def _rotation(alpha, beta, gamma):
+    """Reference symmetric-Schur rotation (reference main.cu:715-725), batched."""
+    safe = torch.where(alpha == 0, torch.ones_like(alpha), alpha)
+    tau = (gamma - beta) / (2 * safe)
+    big = 1e150 if alpha.dtype == torch.float64 else 1e18
+    at = tau.abs()
+    t = torch.where(at > big, 1.0 / (2 * tau), 1.0 / (at + torch.sqrt(1 + torch.clamp(tau * tau, max=1e300 if alpha.dtype == torch.float64 else 3e38))))
+    t = torch.where((at <= big) & (tau < 0), -t, t)
+    c = 1.0 / torch.sqrt(1 + t * t)
+    s = t * c
+    return c, s, t
+
+
+def scalar_step(At, Vt, pairs, tol, tol_mode=0):
+    """One parallel step of the scalar method on disjoint column pairs.
+
+    pairs: int tensor (k, 2) (negative entries skipped).  Returns (maxconv, rotations).
+    """
+    pairs = pairs[(pairs[:, 0] >= 0) & (pairs[:, 1] >= 0)]
+    if pairs.numel() == 0:
+        return 0.0, 0
+    p, q = pairs[:, 0].long(), pairs[:, 1].long()
+    x, y = At[p], At[q]
+    alpha = (x * y).sum(1)
+    beta = (x * x).sum(1)
+    gamma = (y * y).sum(1)
+    nrm = beta.sqrt() * gamma.sqrt()
+    conv = torch.where(nrm > 0, alpha.abs() / torch.where(nrm > 0, nrm, torch.ones_like(nrm)), torch.zeros_like(nrm))
+    if tol_mode == 1:
+        rot = alpha.abs() > tol
+    else:
+        rot = (nrm > 0) & (alpha.abs() > tol * nrm)
+    rot &= alpha != 0
+    maxconv = float(conv.max()) if conv.numel() else 0.0
+    if not bool(rot.any()):
+        return maxconv, 0
+    c, s, _ = _rotation(alpha, beta, gamma)
+    c = torch.where(rot, c, torch.ones_like(c))[:, None]
+    s = torch.where(rot, s, torch.zeros_like(s))[:, None]
+    At[p] = c * x - s * y
+    At[q] = s * x + c * y
+    if Vt is not None:
+        vx, vy = Vt[p], Vt[q]
+        Vt[p] = c * vx - s * vy
+        Vt[q] = s * vx + c * vy
+    return maxconv, int(rot.sum())
+
+
+def round_robin_pairs(N):
+    out = []
+    for r in range(N - 1):
+        prs = [(r, N - 1)]
+        for k in range(1, N // 2):
+            a, b = (r + k) % (N - 1), (r - k + N - 1) % (N - 1)
+            prs.append((min(a, b), max(a, b)))
+        out.append(prs)
+    return out
+
+
+_RR_CACHE = {}
+
+
+def jacobi_evd(G, tol, max_sweeps):
+    """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
+
+    Same round-robin ordering, threshold and update formulas as the LDS
+    kernel (csrc/hip/block.hip evd_kernel).  Returns (G_diag_final, Q, rotated).
+    """
+    G = G.clone()
+    P, N, _ = G.shape
+    Q = torch.eye(N, dtype=G.dtype).expand(P, N, N).clone()
+    sched = _RR_CACHE.get(N)
+    if sched is None:
+        sched = [(torch.tensor([a for a, b in prs]), torch.tensor([b for a, b in prs]))
+                 for prs in round_robin_pairs(N)]
+        _RR_CACHE[N] = sched
+    rotated = torch.zeros(P, dtype=torch.bool)
+    for _ in range(max_sweeps):
+        sweep_rot = torch.zeros(P, dtype=torch.bool)
+        for p, q in sched:
+            gpp, gqq, gpq = G[:, p, p], G[:, q, q], G[:, p, q]
+            nrm = gpp.clamp(min=0).sqrt() * gqq.clamp(min=0).sqrt()
+            rot = (nrm > 0) & (gpq.abs() > tol * nrm)
+            if not bool(rot.any()):
+                continue
+            sweep_rot |= rot.any(1)
+            c, s, t = _rotation(gpq, gpp, gqq)
+            c = torch.where(rot, c, torch.ones_like(c))
+            s = torch.where(rot, s, torch.zeros_like(s))
+            t = torch.where(rot, t, torch.zeros_like(t))
+            Gp, Gq = G[:, p, :].clone(), G[:, q, :].clone()
+            G[:, p, :] = c[:, :, None] * Gp - s[:, :, None] * Gq
+            G[:, q, :] = s[:, :, None] * Gp + c[:, :, None] * Gq
+            Gp, Gq = G[:, :, p].clone(), G[:, :, q].clone()
+            G[:, :, p] = c[:, None, :] * Gp - s[:, None, :] * Gq
+            G[:, :, q] = s[:, None, :] * Gp + c[:, None, :] * Gq
+            # exact diagonal-block update (matches the kernel)
+            G[:, p, p] = gpp - t * gpq
+            G[:, q, q] = gqq + t * gpq
+            G[:, p, q] = torch.where(rot, torch.zeros_like(gpq), G[:, p, q])
+            G[:, q, p] = G[:, p, q]
+            Qp, Qq = Q[:, :, p].clone(), Q[:, :, q].clone()
+            Q[:, :, p] = c[:, None, :] * Qp - s[:, None, :] * Qq
+            Q[:, :, q] = s[:, None, :] * Qp + c[:, None, :] * Qq
+        rotated |= sweep_rot
+        if not bool(sweep_rot.any()):
+            break
+    return torch.diagonal(G, dim1=1, dim2=2).clone(), Q, rotated
+
+
+def block_step(At, Vt, D, pairs, W, full, tol, max_inner):
+    """One block step on P disjoint block pairs (pairs: (P, 2) block ids).
+
+    Mirrors csrc/hip/block.hip (gram -> evd -> apply).  Updates At, Vt, D in
+    place.  Returns (maxconv, pairs_rotated).
+    """
+    P = pairs.shape[0]
+    if P == 0:
+        return 0.0, 0
+    ar = torch.arange(W)
+    ci = pairs[:, 0].long()[:, None] * W + ar
+    cj = pairs[:, 1].long()[:, None] * W + ar
+    cols = torch.cat([ci, cj], 1)  # (P, 2W)
+    X = At[cols]  # (P, 2W, ld)
+    N = 2 * W
+    idx = torch.arange(N)
+    if full:
+        G = X @ X.transpose(1, 2)
+        mask = torch.triu(torch.ones(N, N, dtype=torch.bool), 1)
+    else:
+        C = X[:, :W] @ X[:, W:].transpose(1, 2)
+        G = torch.zeros(P, N, N, dtype=At.dtype)
+        G[:, idx, idx] = D[cols]
+        G[:, :W, W:] = C
+        G[:, W:, :W] = C.transpose(1, 2)
+        mask = torch.zeros(N, N, dtype=torch.bool)
+        mask[:W, W:] = True
+    dg = torch.diagonal(G, dim1=1, dim2=2).clamp(min=0).sqrt()
+    den = dg[:, :, None] * dg[:, None, :]
+    R = torch.where(den > 0, G.abs() / torch.where(den > 0, den, torch.ones_like(den)), torch.zeros_like(den))
+    maxconv = float(R[:, mask].max()) if mask.any() else 0.0
+    lam, Q, rotated = jacobi_evd(G, tol, max_inner)
+    if bool(rotated.any()):
+        sel = rotated
+        Qs = Q[sel]
+        csel = cols[sel]
+        At[csel] = Qs.transpose(1, 2) @ X[sel]
+        if Vt is not None:
+            Vt[csel] = Qs.transpose(1, 2) @ Vt[csel]
+    upd = rotated if not full else torch.ones_like(rotated)
+    if bool(upd.any()):
+        D[cols[upd]] = lam[upd]
+    return maxconv, int(rotated.sum())
+
+
+def col_norms2(At):
+    return (At.double() ** 2).sum(1).to(At.dtype)
+
+
+def finalize(At, scale_u=True):
+    sig = (At.double() ** 2).sum(1).sqrt()
+    if scale_u:
+        nz = sig > 0
+        At[nz] = (At[nz].double() / sig[nz, None]).to(At.dtype)
+    return sig.to(At.dtype)
+
+
+def default_tol(dtype, m):
+    eps = torch.finfo(dtype).eps
+    return 4.0 * math.sqrt(max(m, 1)) * eps

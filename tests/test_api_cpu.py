@@ -1,0 +1,81 @@
+"""Public API on CPU tensors (oracle / torch-reference paths)."""
+import pytest
+import torch
+
+import svdj
+
+
+@pytest.mark.parametrize("method", ["oracle", "scalar", "block"])
+def test_svd_methods_cpu(method):
+    A = svdj.utils.inputs.random_dense(100, 64, seed=2)
+    res = svdj.svd(A, method=method, dtype=torch.float64)
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert res.converged
+    assert rep["residual_rel"] < 1e-12 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
+    assert res.U.shape == (100, 64) and res.V.shape == (64, 64) and res.S.shape == (64,)
+
+
+def test_wide_matrix_transposes():
+    A = svdj.utils.inputs.random_dense(40, 70, seed=4)
+    res = svdj.svd(A)
+    assert res.info.get("transposed")
+    assert res.U.shape == (40, 40) and res.V.shape == (70, 40)
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-12
+
+
+def test_sort_and_novec():
+    A = svdj.utils.inputs.random_dense(50, 50, seed=5)
+    res = svdj.svd(A, sort=True)
+    assert torch.all(res.S[:-1] >= res.S[1:])
+    r2 = svdj.svd(A, jobu=svdj.NoVec, jobv=svdj.NoVec)
+    assert r2.U is None and r2.V is None
+    torch.testing.assert_close(torch.sort(r2.S, descending=True).values, res.S)
+
+
+def test_known_spectrum_graded():
+    s = svdj.utils.inputs.geometric_spectrum(64, 1e8)
+    A = svdj.utils.inputs.with_spectrum(80, 64, s)
+    res = svdj.svd(A, method="oracle", sort=True)
+    rel = ((res.S - s).abs() / s).max()
+    assert rel < 1e-7  # one-sided Jacobi: relative accuracy on graded spectra
+
+
+def test_gesvd_inplace_cpu():
+    n, lda = 48, 64
+    A = svdj.utils.inputs.random_dense(n, n, seed=6)
+    buf = torch.zeros(lda * n, dtype=torch.float64)
+    buf.view(n, lda)[:, :n] = A.t()
+    s = torch.zeros(n, dtype=torch.float64)
+    V = torch.zeros(n * n, dtype=torch.float64)
+    svdj.gesvd(svdj.AllVec, svdj.AllVec, n, n, buf, lda, s, V, n)
+    U = buf.view(n, lda)[:, :n].t()
+    rep = svdj.utils.metrics.verify(A, U, s, V.view(n, n).t(), torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-12
+
+
+def test_options_parse():
+    assert svdj.SVDOptions.parse("A") == svdj.AllVec
+    assert svdj.SVDOptions.parse("some") == svdj.SomeVec
+    assert svdj.SVDOptions.parse(2) == svdj.NoVec
+    with pytest.raises(ValueError):
+        svdj.SVDOptions.parse("bogus")
+
+
+def test_reference_ops_block_step_orthogonalises_pair():
+    R = svdj.ops.reference
+    W, m = 8, 50
+    At = torch.rand(4 * W, m, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    Vt = torch.eye(4 * W, dtype=torch.float64)
+    D = (At ** 2).sum(1)
+    A0 = At.clone()
+    mx, nrot = R.block_step(At, Vt, D, torch.tensor([[0, 1], [2, 3]]), W, True, 1e-14, 30)
+    assert nrot == 2 and mx > 0.1
+    G = At @ At.t()
+    for blk in ([0, 1], [2, 3]):
+        cols = torch.cat([torch.arange(b * W, (b + 1) * W) for b in blk])
+        g = G[cols][:, cols]
+        off = g - torch.diag(torch.diagonal(g))
+        assert off.abs().max() < 1e-10 * g.diagonal().max()
+    torch.testing.assert_close(Vt @ A0, At, atol=1e-12, rtol=0)  # A_new = A_old V (Vt rows = V cols)
+    torch.testing.assert_close(D, torch.diagonal(G), rtol=1e-10, atol=1e-12)

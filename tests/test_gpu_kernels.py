@@ -1,0 +1,142 @@
+"""HIP kernel numerics vs plain-PyTorch fp64 references (needs MI355X)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_At(ncols, m_pad, m, dtype, device, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    At = torch.zeros(ncols, m_pad, dtype=torch.float64)
+    At[:, :m] = torch.rand(ncols, m, generator=g, dtype=torch.float64) - 0.3
+    return At.to(dtype).to(device)
+
+
+def test_native_loaded(svdj, cuda):
+    lib = svdj.ops.hip_lib()
+    assert b"gfx950" in lib.svdj_hip_version()
+    assert torch.cuda.get_device_properties(0).gcnArchName.startswith("gfx950")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_col_norms_finalize_identity(svdj, cuda, dtype):
+    K = svdj.ops.kernels
+    At = _rand_At(40, 256, 200, dtype, cuda)
+    D = K.col_norms2(At, 256)
+    ref = (At.double().cpu() ** 2).sum(1)
+    torch.testing.assert_close(D.double().cpu(), ref, rtol=1e-5 if dtype == torch.float32 else 1e-12, atol=0)
+    A0 = At.double().cpu().clone()
+    s = K.finalize(At, 256, True)
+    torch.testing.assert_close(s.double().cpu(), ref.sqrt(), rtol=1e-6 if dtype == torch.float32 else 1e-13, atol=0)
+    torch.testing.assert_close(At.double().cpu(), A0 / ref.sqrt()[:, None], rtol=1e-5 if dtype == torch.float32 else 1e-12, atol=1e-7)
+    V = torch.full((40, 128), 7.0, dtype=dtype, device=cuda)
+    K.set_identity(V, 40)
+    assert torch.equal(V.cpu(), torch.eye(40, 128, dtype=dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_scalar_step_matches_reference(svdj, cuda, dtype):
+    K = svdj.ops.kernels
+    R = svdj.ops.reference
+    n, m, m_pad = 32, 300, 384
+    At = _rand_At(n, m_pad, m, dtype, cuda, seed=1)
+    Vt = torch.eye(n, 128, dtype=dtype, device=cuda)
+    sched = torch.from_numpy(svdj.parallel.schedule.sameh(n)).to(cuda)
+    At_ref, Vt_ref = At.double().cpu(), Vt.double().cpu()
+    metric = K.new_metric(cuda)
+    tol = 1e-7
+    for s in range(3):
+        K.scalar_step(At, Vt, m_pad, sched[s], tol, 0, metric)
+        R.scalar_step(At_ref, Vt_ref, sched[s].cpu(), tol, 0)
+    mx, nrot = K.read_metric(metric)
+    assert nrot == 3 * (n // 2)
+    assert 0 < mx <= 1
+    tol_cmp = 2e-5 if dtype == torch.float32 else 1e-12
+    torch.testing.assert_close(At.double().cpu(), At_ref, rtol=tol_cmp, atol=tol_cmp)
+    torch.testing.assert_close(Vt.double().cpu(), Vt_ref, rtol=tol_cmp, atol=tol_cmp)
+
+
+@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64), (torch.float64, 32)])
+@pytest.mark.parametrize("full", [1, 0])
+def test_block_step_matches_reference(svdj, cuda, dtype, W, full):
+    """One gram -> evd -> apply step vs the fp64 torch reference on the same input."""
+    K = svdj.ops.kernels
+    R = svdj.ops.reference
+    nb = 4
+    n, m, m_pad = nb * W, 500, 512
+    At = _rand_At(n, m_pad, m, dtype, cuda, seed=2)
+    if not full:
+        # cross mode assumes blocks internally orthogonal: orthogonalise each block
+        A64 = At.double().cpu()
+        for b in range(nb):
+            blk = A64[b * W:(b + 1) * W, :m]
+            q, r = torch.linalg.qr(blk.t())
+            A64[b * W:(b + 1) * W, :m] = (q * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+        At = A64.to(dtype).to(cuda)
+    Vt = torch.zeros(n, 256, dtype=dtype, device=cuda)
+    K.set_identity(Vt, n)
+    D = K.col_norms2(At, m_pad)
+    pairs = torch.tensor([[[0, 3], [1, 2]]], dtype=torch.int32)
+    At64, Vt64, D64 = At.double().cpu(), Vt.double().cpu(), D.double().cpu()
+    tol = 1e-6 if dtype == torch.float32 else 1e-13
+    metric = K.new_metric(cuda)
+    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [full], tol, 12, metric)
+    mx_ref, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, bool(full), tol, 12)
+    mx, nrot = K.read_metric(metric)
+    assert nrot == nrot_ref == 2
+    assert math.isclose(mx, mx_ref, rel_tol=1e-3)
+    # Columns of the rotated panels must be mutually orthogonal and span the
+    # same space as the reference: compare the invariants, not the (sign /
+    # order ambiguous) individual columns.
+    Ag = At.double().cpu()
+    for bi, bj in pairs[0].tolist():
+        cols = list(range(bi * W, bi * W + W)) + list(range(bj * W, bj * W + W))
+        X = Ag[cols, :m]
+        G = X @ X.t()
+        off = G - torch.diag(torch.diagonal(G))
+        dg = torch.diagonal(G).sqrt()
+        rel = (off.abs() / (dg[:, None] * dg[None, :])).max()
+        assert rel < (5e-5 if dtype == torch.float32 else 1e-11), rel
+        # squared norms tracked in D equal the data's
+        torch.testing.assert_close(D.double().cpu()[cols], torch.diagonal(G), rtol=1e-4 if dtype == torch.float32 else 1e-10, atol=1e-6)
+        # same singular values of the pair panel
+        torch.testing.assert_close(torch.sort(torch.diagonal(G)).values, torch.sort(D64[cols]).values,
+                                   rtol=1e-4 if dtype == torch.float32 else 1e-10, atol=1e-6)
+        # A V = A0 V0 relation: X_new = X_old Q => X_new^T X_new eigenvalues
+    # V stays orthogonal and A_new = A_old_full * V (columns) holds
+    Vg = Vt.double().cpu()
+    # fp32 W=32 accumulates Q in fp64 (orthogonal to ~eps); fp32 W=64 in fp32.
+    vtol = {(torch.float32, 32): 2e-6, (torch.float32, 64): 5e-5}.get((dtype, W), 1e-13)
+    torch.testing.assert_close(Vg[:, :n] @ Vg[:, :n].t(), torch.eye(n, dtype=torch.float64),
+                               rtol=0, atol=vtol)
+
+
+@pytest.mark.parametrize("method,dtype", [("block", torch.float32), ("block", torch.float64),
+                                          ("scalar", torch.float32), ("scalar", torch.float64)])
+def test_svd_end_to_end(svdj, cuda, method, dtype):
+    m, n = 520, 384
+    A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=3)
+    res = svdj.svd(A.to(cuda), method=method, dtype=dtype)
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
+    eps = torch.finfo(dtype).eps
+    assert rep["residual_rel"] < 2000 * eps, rep
+    assert rep["sigma_max_abs_err_over_smax"] < 2000 * eps, rep
+    assert rep["orth_u_fro"] < 50 * math.sqrt(n) * 4 * math.sqrt(m) * eps * 10, rep
+    assert rep["orth_v_fro"] < 2e4 * math.sqrt(n) * eps, rep
+
+
+def test_gesvd_inplace_reference_signature(svdj, cuda):
+    n = 256
+    A = svdj.utils.inputs.reference_dense(n).to(cuda)  # column-major view of a buffer
+    buf = A.t().contiguous().reshape(-1).clone()  # column-major storage, lda = n
+    s = torch.zeros(n, dtype=torch.float64, device=cuda)
+    V = torch.zeros(n * n, dtype=torch.float64, device=cuda)
+    res = svdj.gesvd(svdj.AllVec, svdj.AllVec, n, n, buf, n, s, V, n)
+    U = buf.view(n, n).t()
+    Vm = V.view(n, n).t()
+    rep = svdj.utils.metrics.verify(A, U, s, Vm, torch.linalg.svdvals(A.cpu()))
+    assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-9, rep
+    assert res.sweeps >= 2

@@ -1,0 +1,12 @@
+set -o pipefail
+export SVDJ_NO_AUTOBUILD=1
+R=$GRAFT_REPO_ROOT
+timeout -k 10 400 python -m pytest tests -m gpu -q > gpurun_out/gpu_tests.log 2>&1; echo "pytest rc=$?" >> gpurun_out/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || echo smoke-failed >> gpurun_out/smoke.log
+timeout -k 10 300 python tools/quick_perf.py --sizes 2048,4096 --block 32 --verify > gpurun_out/perf_w32.log 2>&1
+timeout -k 10 300 python tools/quick_perf.py --sizes 4096 --block 64 --verify > gpurun_out/perf_w64.log 2>&1
+timeout -k 10 300 python tools/quick_perf.py --sizes 2048 --dtype fp64 --verify > gpurun_out/perf_f64.log 2>&1
+timeout -k 10 400 python bench.py --n 8192 --steps 1 --warmup 1 > gpurun_out/bench_8192.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof3 -o run --output-format csv -- python $R/tools/quick_perf.py --sizes 4096 --block 32 > $R/gpurun_out/prof3.log 2>&1
+cd $R; tail -3 gpurun_out/gpu_tests.log; cat gpurun_out/smoke.log gpurun_out/perf_*.log gpurun_out/bench_8192.log | grep -v amdgpu.ids
