@@ -94,6 +94,18 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 4) -> Path
     return HIP_LIB
 
 
+def build_hip_variant(name: str, defines: list, verbose: bool = False) -> Path:
+    """Build an A/B variant of the HIP library (extra -D flags) under lib/variants/."""
+    hipcc = _hipcc()
+    out_dir = LIBDIR / "variants"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    out = out_dir / f"libsvdj_hip_{name}.so"
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-shared",
+             f"-I{CSRC / 'include'}", f"-I{CSRC / 'hip'}", *[f"-D{d}" for d in defines]]
+    _run([hipcc, *flags, *HIP_SOURCES, "-o", out], verbose)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = False) -> dict:
     return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose))}
 

@@ -171,7 +171,15 @@ __device__ __forceinline__ void rr_pair(int st, int a, int N, int& p, int& q) {
 //     16/32-byte record, barrier, then G blocks are updated from the records
 //     while the fp64 (c, s) for Q are formed from t off the critical path
 //     (c^2 + s^2 = 1 to fp64 accuracy), barrier, DPP shift.
-__host__ __device__ constexpr int evd_threads(int W) { return W == 64 ? 1024 : 512; }
+#ifndef SVDJ_EVD_THREADS_32
+#define SVDJ_EVD_THREADS_32 512
+#endif
+#ifndef SVDJ_EVD_THREADS_64
+#define SVDJ_EVD_THREADS_64 1024
+#endif
+__host__ __device__ constexpr int evd_threads(int W) {
+  return W == 64 ? SVDJ_EVD_THREADS_64 : SVDJ_EVD_THREADS_32;
+}
 
 __device__ __forceinline__ int dpp_shr1(int v) {
   return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);  // lane i <- lane i-1
@@ -190,11 +198,44 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Per-slot rotation record published by wave 0 each step: (c, s) in fp64
+// for the Q accumulation, (c, s, t) in the data precision for G, players.
 template <typename T>
-struct alignas(sizeof(T) == 8 ? 32 : 16) RotRec {
+struct alignas(16) RotRec {
+  double c64, s64;
   T c, s, t;
   int pq;  // p | q << 16
 };
+
+// Fast fp32 rotation (raw v_sqrt/v_rcp/v_rsq, ~1 ulp): only steers G; Q is
+// built from the fp64-normalised (c, s).
+__device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, float tol,
+                                              float& c, float& s, float& t) {
+  const float nrm = __builtin_amdgcn_sqrtf(gpp) * __builtin_amdgcn_sqrtf(gqq);
+  if (!(nrm > 0.0f) || !(fabsf(gpq) > tol * nrm)) return false;
+  const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * gpq);
+  const float at = fabsf(tau);
+  float tt = at > 1e18f ? 0.5f * __builtin_amdgcn_rcpf(at)
+                        : __builtin_amdgcn_rcpf(at + __builtin_amdgcn_sqrtf(1.0f + tau * tau));
+  t = tau < 0.0f ? -tt : tt;
+  c = __builtin_amdgcn_rsqf(1.0f + t * t);
+  s = t * c;
+  return true;
+}
+__device__ __forceinline__ bool rotation_fast(double gpp, double gqq, double gpq, double tol,
+                                              double& c, double& s, double& t) {
+  const double nrm = sqrt(gpp) * sqrt(gqq);
+  if (!(nrm > 0.0) || !(fabs(gpq) > tol * nrm)) return false;
+  schur_rotation<double>(gpq, gpp, gqq, c, s, t);
+  return true;
+}
+// fp64 1/sqrt(x) for x in [1, 2^60]: hardware estimate + 2 Newton steps.
+__device__ __forceinline__ double rsqrt64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * (1.5 - 0.5 * x * y * y);
+  y = y * (1.5 - 0.5 * x * y * y);
+  return y;
+}
 
 template <typename T, int W>
 __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
@@ -304,20 +345,29 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   bool any = false;
   for (int sw = 0; sw < max_inner; ++sw) {
     for (int st = 0; st < N - 1; ++st) {
-      // (1) every lane solves its slot's rotation in the data precision
-      const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[sidx(pf, ps)];
-      const T nrm = sqrt(gpp) * sqrt(gqq);
-      const bool rot = nrm > T(0) && fabs(gpq) > tol * nrm;
-      T c = 1, s = 0, t = 0;
-      if (rot) schur_rotation<T>(gpq, gpp, gqq, c, s, t);
+      // (1) wave 0 solves the W rotations of this step and publishes them
       if (wave == 0 && lane < W) {
+        const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[sidx(pf, ps)];
+        T c = 1, s = 0, t = 0;
         RotRec<T> r;
+        r.c64 = 1.0;
+        r.s64 = 0.0;
+        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) {
+          if constexpr (sizeof(T) == 8) {
+            r.c64 = c;
+            r.s64 = s;
+          } else {
+            const double td = (double)t;
+            r.c64 = rsqrt64(1.0 + td * td);
+            r.s64 = td * r.c64;
+          }
+          sweep_rot = 1;
+        }
         r.c = c;
         r.s = s;
         r.t = t;
         r.pq = pf | (ps << 16);
         prm[slot] = r;
-        if (rot) sweep_rot = 1;
       }
       __syncthreads();
       // (2) G <- J^T G J on this thread's upper-triangle 2x2 blocks
@@ -347,22 +397,16 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
           G[i11] = B.s * h10 + B.c * h11;
         }
       }
-      // (3) Q <- Q J in registers (fp64 rotation, normalised from t)
-      if (rot) {
-        double c64, s64;
-        if constexpr (sizeof(T) == 8) {
-          c64 = c;
-          s64 = s;
-        } else {
-          const double td = (double)t;
-          c64 = 1.0 / sqrt(1.0 + td * td);
-          s64 = td * c64;
-        }
+      // (3) Q <- Q J in registers (fp64)
+      {
+        const double c64 = prm[slot].c64, s64 = prm[slot].s64;
+        if (s64 != 0.0) {
 #pragma unroll
-        for (int i = 0; i < RPL; ++i) {
-          const double x = qf[i], y = qs[i];
-          qf[i] = c64 * x - s64 * y;
-          qs[i] = s64 * x + c64 * y;
+          for (int i = 0; i < RPL; ++i) {
+            const double x = qf[i], y = qs[i];
+            qf[i] = c64 * x - s64 * y;
+            qs[i] = s64 * x + c64 * y;
+          }
         }
       }
       __syncthreads();
@@ -536,9 +580,37 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
-  return ((slabs + 255) / 256 * 256) + ((q + 255) / 256 * 256) + ((sk + 255) / 256 * 256);
+  // slabs + double-buffered Q and skip flags (V update runs one step behind)
+  return ((slabs + 255) / 256 * 256) + 2 * ((q + 255) / 256 * 256) + 2 * ((sk + 255) / 256 * 256);
 }
 
+// Side stream + events for the deferred V update (one set per device).
+struct SideStream {
+  hipStream_t sv = nullptr;
+  hipEvent_t ev_q[2] = {nullptr, nullptr};
+  hipEvent_t ev_v[2] = {nullptr, nullptr};
+};
+static SideStream* side_stream() {
+  static thread_local SideStream cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  SideStream& s = cache[dev];
+  if (s.sv == nullptr) {
+    if (hipStreamCreateWithFlags(&s.sv, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (int i = 0; i < 2; ++i) {
+      if (hipEventCreateWithFlags(&s.ev_q[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s.ev_v[i], hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    }
+  }
+  return &s;
+}
+
+// Step pipeline.  Main stream: gram(s) -> evd(s) -> apply_A(s).  The V
+// update of step s only feeds the final result, so it runs on a side stream
+// (waiting for evd(s)) and overlaps gram/evd/apply_A of step s+1; Q and the
+// skip flags are double-buffered, and evd(s+2) waits for apply_V(s) before
+// reusing its buffer.  The caller's stream joins the side stream at the end.
 template <typename T, int W>
 static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
                          const int32_t* pairs, int P, int steps, const int32_t* modes,
@@ -553,10 +625,28 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
   char* w = (char*)ws;
   T* slabs = (T*)w;
   w += ((size_t)P * g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
-  T* Q = (T*)w;
-  w += ((size_t)P * 4 * W * W * sizeof(T) + 255) / 256 * 256;
-  int32_t* skip = (int32_t*)w;
+  const size_t qstride = ((size_t)P * 4 * W * W * sizeof(T) + 255) / 256 * 256;
+  T* Qb[2] = {(T*)w, (T*)(w + qstride)};
+  w += 2 * qstride;
+  const size_t kstride = ((size_t)P * sizeof(int32_t) + 255) / 256 * 256;
+  int32_t* skipb[2] = {(int32_t*)w, (int32_t*)(w + kstride)};
+#ifdef SVDJ_V_OVERLAP
+  SideStream* ss = V ? side_stream() : nullptr;
+#else
+  SideStream* ss = nullptr;
+#endif
+  // Measured on MI355X (n=4096, W=32): the side-stream V update does not
+  // overlap usefully with the latency-bound EVD (152 vs 160 us/step), so it
+  // is opt-in (-DSVDJ_V_OVERLAP) until the EVD is restructured.
+#ifdef SVDJ_V_OVERLAP
+  const bool overlap = ss != nullptr && steps > 1;
+#else
+  const bool overlap = false;
+#endif
   for (int s = 0; s < steps; ++s) {
+    const int b = s & 1;
+    T* Q = Qb[b];
+    int32_t* skip = skipb[b];
     const int32_t* pr = pairs + (size_t)s * P * 2;
     const int full = modes ? modes[s] : 0;
     if (full)
@@ -566,14 +656,29 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
       hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(P, g.gchunks), dim3(kGramThreads), 0,
                          st, A, lda, m_pad, pr, g.grows, slabs);
     SVDJ_LAUNCH_CHECK();
+    if (overlap && s >= 2) SVDJ_HIP_CHECK(hipStreamWaitEvent(st, ss->ev_v[b], 0));
     hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full, slabs,
                        g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
-    hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks + g.v_chunks),
-                       dim3(kApplyThreads), 0, st, A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv,
-                       g.rows_v, V ? n_v : 0, pr, Q, skip);
-    SVDJ_LAUNCH_CHECK();
+    if (overlap) {
+      SVDJ_HIP_CHECK(hipEventRecord(ss->ev_q[b], st));
+      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks), dim3(kApplyThreads), 0, st,
+                         A, lda, g.a_chunks, g.rows_a, m_pad, (T*)nullptr, ldv, g.rows_v, 0, pr,
+                         Q, skip);
+      SVDJ_LAUNCH_CHECK();
+      SVDJ_HIP_CHECK(hipStreamWaitEvent(ss->sv, ss->ev_q[b], 0));
+      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.v_chunks), dim3(kApplyThreads), 0, ss->sv,
+                         V, ldv, 0, g.rows_a, m_pad, V, ldv, g.rows_v, n_v, pr, Q, skip);
+      SVDJ_LAUNCH_CHECK();
+      SVDJ_HIP_CHECK(hipEventRecord(ss->ev_v[b], ss->sv));
+    } else {
+      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks + g.v_chunks),
+                         dim3(kApplyThreads), 0, st, A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv,
+                         g.rows_v, V ? n_v : 0, pr, Q, skip);
+      SVDJ_LAUNCH_CHECK();
+    }
   }
+  if (overlap) SVDJ_HIP_CHECK(hipStreamWaitEvent(st, ss->ev_v[(steps - 1) & 1], 0));
   return 0;
 }
 
