@@ -106,8 +106,28 @@ def build_hip_variant(name: str, defines: list, verbose: bool = False) -> Path:
     return out
 
 
+DRIVER_SRC = CSRC / "driver" / "svdj_main.cpp"
+DRIVER_BIN = PKG / "bin" / "svdj_main"
+
+
+def build_driver(force: bool = False, verbose: bool = False) -> Path:
+    """Native single-GPU driver (reference `SVD_Jacobi_MPI_CUDA <n>` parity),
+    linked against the two in-tree libraries with an $ORIGIN rpath."""
+    cpu, hip = build_cpu(force, verbose), build_hip(force, verbose)
+    DRIVER_BIN.parent.mkdir(exist_ok=True)
+    if not force and not _stale(DRIVER_BIN, [DRIVER_SRC, cpu, hip] + HEADERS):
+        return DRIVER_BIN
+    tmp = DRIVER_BIN.with_suffix(".tmp")
+    _run([_hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", f"-I{CSRC / 'include'}",
+          DRIVER_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_hip", "-lsvdj_cpu",
+          "-Wl,-rpath,$ORIGIN/../lib"], verbose)
+    os.replace(tmp, DRIVER_BIN)
+    return DRIVER_BIN
+
+
 def build_all(force: bool = False, verbose: bool = False) -> dict:
-    return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose))}
+    return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose)),
+            "driver": str(build_driver(force, verbose))}
 
 
 if __name__ == "__main__":

@@ -51,6 +51,7 @@ class SolverConfig:
     max_sweeps: int = 60            # reference: 1 (main.cu:482)
     max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)
     ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
+    rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
     use_graph: bool = False
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)

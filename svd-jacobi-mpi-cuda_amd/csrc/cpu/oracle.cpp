@@ -50,6 +50,30 @@ inline void rotation_params(T alpha, T beta, T gamma, T& c, T& s) {
   s = t * c;
 }
 
+// "Ordered" one-sided rotation (Erricos, Handbook of Parallel Computing and
+// Statistics p.128; reference lib/Utils.cu:57-80, compiled there but never
+// called).  xi = 2 a_p.a_q, beta = ||a_p||^2 - ||a_q||^2 (the reference's
+// comment says ||a_q||^2; the difference is what makes the formula orthogonalise),
+// gamma = sqrt(xi^2 + beta^2).  Applied as a_p' = c a_p + s a_q,
+// a_q' = -s a_p + c a_q it also moves the larger norm into column p, so the
+// sweep tends to leave sigma sorted.  Returned in this file's convention
+// (x' = c x - s y) i.e. with s negated.
+template <typename T>
+inline void rotation_params_ordered(T alpha, T np2, T nq2, T& c, T& s) {
+  const T xi = T(2) * alpha;
+  const T beta = np2 - nq2;
+  const T gamma = std::sqrt(xi * xi + beta * beta);
+  T so;
+  if (beta > T(0)) {
+    c = std::sqrt((beta + gamma) / (T(2) * gamma));
+    so = xi / (T(2) * gamma * c);
+  } else {
+    so = std::sqrt((gamma - beta) / (T(2) * gamma));
+    c = xi / (T(2) * gamma * so);
+  }
+  s = -so;
+}
+
 template <typename T>
 int jacobi_impl(int jobu, int jobv, int m, int n, T* A, int lda, T* s, T* V,
                 int ldv, int ordering, int max_sweeps, double tol, int tol_mode,
@@ -69,6 +93,10 @@ int jacobi_impl(int jobu, int jobv, int m, int n, T* A, int lda, T* s, T* V,
       col[j] = T(1);
     }
   }
+  // ordering: bits 0-3 schedule (0 Sameh, 1 round robin),
+  //           bits 4-7 rotation formula (0 symmetric Schur, 1 ordered).
+  const int rot_kind = (ordering >> 4) & 0xF;
+  ordering &= 0xF;
   // Schedule.
   int steps, per_step;
   std::vector<int32_t> sched;
@@ -87,12 +115,22 @@ int jacobi_impl(int jobu, int jobv, int m, int n, T* A, int lda, T* s, T* V,
       if (x >= n) x = -1;  // dummy column for odd n
   }
   int sweeps = 0;
-  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    double maxconv = 0.0;
-    long rotations = 0;
+  // One parallel region for the whole solve (a fork/join per step costs more
+  // than the step itself for small n); each step is an `omp for` whose
+  // implicit barrier orders the steps.
+  double maxconv = 0.0;
+  long rotations = 0;
+  bool done = false;
+#pragma omp parallel
+  for (int sweep = 0; sweep < max_sweeps && !done; ++sweep) {
+#pragma omp single
+    {
+      maxconv = 0.0;
+      rotations = 0;
+    }
     for (int st = 0; st < steps; ++st) {
       const int32_t* pr = sched.data() + (size_t)st * per_step * 2;
-#pragma omp parallel for schedule(static) reduction(max : maxconv) reduction(+ : rotations)
+#pragma omp for schedule(static) reduction(max : maxconv) reduction(+ : rotations)
       for (int k = 0; k < per_step; ++k) {
         const int p = pr[2 * k], q = pr[2 * k + 1];
         if (p < 0 || q < 0) continue;
@@ -117,7 +155,10 @@ int jacobi_impl(int jobu, int jobv, int m, int n, T* A, int lda, T* s, T* V,
           rotate = nrm > T(0) && std::fabs(alpha) > T(tol) * nrm;
         if (!rotate || alpha == T(0)) continue;
         T c, sn;
-        rotation_params(alpha, beta, gamma, c, sn);
+        if (rot_kind == 1)
+          rotation_params_ordered(alpha, beta, gamma, c, sn);
+        else
+          rotation_params(alpha, beta, gamma, c, sn);
         ++rotations;
         for (int i = 0; i < m; ++i) {
           const T x = ap[i], y = aq[i];
@@ -135,9 +176,12 @@ int jacobi_impl(int jobu, int jobv, int m, int n, T* A, int lda, T* s, T* V,
         }
       }
     }
-    if (hist) hist[sweep] = maxconv;
-    sweeps = sweep + 1;
-    if (rotations == 0) break;
+#pragma omp single
+    {
+      if (hist) hist[sweep] = maxconv;
+      sweeps = sweep + 1;
+      if (rotations == 0) done = true;
+    }
   }
   // Sigma and U (reference main.cu:1394-1421, with sigma=0 guard).
   const int k = std::min(m, n);

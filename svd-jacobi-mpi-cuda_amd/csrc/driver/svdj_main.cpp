@@ -1,0 +1,176 @@
+// Native single-GPU driver: the reference's `SVD_Jacobi_MPI_CUDA <n>` binary
+// (reference main.cu:1426-1676) rebuilt on the framework's C ABI, with no
+// Python in the loop.  Multi-GPU runs use the Python/RCCL launcher
+// (tools/svd_jacobi.py under torchrun) -- one process per GPU.
+//
+//   svdj_main N [--m M] [--input triu|dense] [--seed S] [--dtype f32|f64]
+//               [--method block|scalar] [--block W] [--max-sweeps K]
+//               [--tol T] [--verify] [--report-dir DIR]
+//
+// Prints the reference's lines ("Dimensions, height: .., width: ..",
+// "SVD MPI+OMP time with U,V calculation: ..", "||A-USVt||_F: ..") and writes
+// reporte-dimension-<n>-time-<ts>.txt.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <vector>
+
+#include "svdj_cpu.h"
+#include "svdj_hip.h"
+
+#define CHECK(x)                                                                  \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      std::fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_),      \
+                   __FILE__, __LINE__);                                           \
+      std::exit(2);                                                               \
+    }                                                                             \
+  } while (0)
+
+static int rup(int a, int b) { return (a + b - 1) / b * b; }
+
+template <typename T>
+static int run(int m, int n, const std::vector<double>& A0, const std::string& method, int W,
+               int max_sweeps, double tol, bool verify, const std::string& report_dir) {
+  const int dtype = sizeof(T) == 8 ? 1 : 0;
+  const bool block = method == "block";
+  const int ncols = block ? std::max(rup(n, 2 * W), 2 * W) : n;
+  const int m_pad = rup(std::max(m, 1), SVDJ_ROW_ALIGN);
+  const int n_v = rup(ncols, SVDJ_ROW_ALIGN);
+  std::vector<T> hA((size_t)ncols * m_pad, T(0));
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) hA[(size_t)j * m_pad + i] = (T)A0[(size_t)j * m + i];
+  T *dA, *dV, *dD, *dS;
+  uint32_t* dmetric;
+  CHECK(hipMalloc(&dA, hA.size() * sizeof(T)));
+  CHECK(hipMalloc(&dV, (size_t)ncols * n_v * sizeof(T)));
+  CHECK(hipMalloc(&dD, (size_t)ncols * sizeof(T)));
+  CHECK(hipMalloc(&dS, (size_t)ncols * sizeof(T)));
+  CHECK(hipMalloc(&dmetric, 2 * sizeof(uint32_t)));
+  CHECK(hipMemcpy(dA, hA.data(), hA.size() * sizeof(T), hipMemcpyHostToDevice));
+  hipStream_t st;
+  CHECK(hipStreamCreate(&st));
+  std::vector<double> hist(max_sweeps, 0.0);
+  if (tol <= 0) tol = 4.0 * std::sqrt((double)m) * (sizeof(T) == 8 ? 2.220446049250313e-16 : 1.1920929e-07);
+
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0, st));
+  int sweeps = 0;
+  void* ws = nullptr;
+  int32_t* dsched = nullptr;
+  if (svdj_set_identity(dtype, dV, n_v, n_v, ncols, 0, st) < 0) goto fail;
+  if (block) {
+    const size_t wsb = svdj_block_workspace_bytes(dtype, W, ncols / W / 2, m_pad);
+    CHECK(hipMalloc(&ws, wsb));
+    if (svdj_col_norms2(dtype, dA, m_pad, m_pad, ncols, dD, st) < 0) goto fail;
+    sweeps = svdj_block_solve(dtype, W, m_pad, dA, m_pad, dV, n_v, n_v, dD, ncols, tol, 1,
+                              max_sweeps, ws, wsb, dmetric, hist.data(), 0, st);
+  } else {
+    const int steps = svdj_sameh_num_steps(n);
+    std::vector<int32_t> sched((size_t)steps * (n / 2) * 2);
+    svdj_sameh_schedule(n, sched.data());
+    CHECK(hipMalloc(&dsched, sched.size() * sizeof(int32_t)));
+    CHECK(hipMemcpy(dsched, sched.data(), sched.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    sweeps = svdj_scalar_solve(dtype, m_pad, dA, m_pad, dV, n_v, n_v, dsched, steps, n / 2, tol,
+                               0, max_sweeps, dmetric, hist.data(), st);
+  }
+  if (sweeps < 0) goto fail;
+  if (svdj_finalize(dtype, dA, m_pad, m_pad, ncols, dS, 1, st) < 0) goto fail;
+  CHECK(hipEventRecord(e1, st));
+  CHECK(hipEventSynchronize(e1));
+  {
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double secs = ms / 1e3;
+    std::printf("SVD MPI+OMP time with U,V calculation: %.6f\n", secs);
+    std::printf("sweeps: %d  last off value: %.3e  tol: %.3e\n", sweeps,
+                sweeps > 0 ? hist[sweeps - 1] : 0.0, tol);
+    const double flops = (double)n * (n - 1) / 2.0 * (12.0 * m + 6.0 * n) * sweeps;
+    std::printf("GFLOP/s (algorithmic): %.1f\n", flops / secs / 1e9);
+    double resid = -1.0;
+    if (verify) {
+      std::vector<T> hU((size_t)ncols * m_pad), hV((size_t)ncols * n_v), hS(ncols);
+      CHECK(hipMemcpy(hU.data(), dA, hU.size() * sizeof(T), hipMemcpyDeviceToHost));
+      CHECK(hipMemcpy(hV.data(), dV, hV.size() * sizeof(T), hipMemcpyDeviceToHost));
+      CHECK(hipMemcpy(hS.data(), dS, hS.size() * sizeof(T), hipMemcpyDeviceToHost));
+      std::vector<double> U((size_t)n * m), V((size_t)n * n), S(n);
+      for (int j = 0; j < n; ++j) {
+        S[j] = hS[j];
+        for (int i = 0; i < m; ++i) U[(size_t)j * m + i] = hU[(size_t)j * m_pad + i];
+        for (int i = 0; i < n; ++i) V[(size_t)j * n + i] = hV[(size_t)j * n_v + i];
+      }
+      resid = svdj_cpu_residual_f64(m, n, n, A0.data(), m, U.data(), m, S.data(), V.data(), n, 0);
+      const double ou = svdj_cpu_orth_f64(m, n, U.data(), m, 0);
+      const double ov = svdj_cpu_orth_f64(n, n, V.data(), n, 0);
+      std::printf("||A-USVt||_F: %.6e\n||U^TU-I||_F: %.3e\n||V^TV-I||_F: %.3e\n", resid, ou, ov);
+    }
+    if (!report_dir.empty()) {
+      char ts[64];
+      std::time_t t = std::time(nullptr);
+      std::strftime(ts, sizeof(ts), "%d-%m-%Y-%H-%M-%S", std::localtime(&t));
+      std::string path = report_dir + "/reporte-dimension-" + std::to_string(m) + "-time-" + ts + ".txt";
+      if (FILE* f = std::fopen(path.c_str(), "w")) {
+        std::fprintf(f, "Number of threads: 1\nDimensions, height: %d, width: %d\n", m, n);
+        std::fprintf(f, "SVD MPI+OMP time with U,V calculation: %.6f\n", secs);
+        if (resid >= 0) std::fprintf(f, "||A-USVt||_F: %.6e\n", resid);
+        std::fclose(f);
+        std::printf("report: %s\n", path.c_str());
+      }
+    }
+  }
+  (void)hipFree(dA); (void)hipFree(dV); (void)hipFree(dD); (void)hipFree(dS);
+  (void)hipFree(dmetric); (void)hipFree(ws); (void)hipFree(dsched);
+  return 0;
+fail:
+  std::fprintf(stderr, "svdj error: %s\n", svdj_hip_last_error());
+  return 3;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s N [--m M] [--input triu|dense] [--dtype f32|f64] ...\n", argv[0]);
+    return 1;
+  }
+  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60;
+  unsigned seed = 1000000;
+  double tol = -1;
+  bool verify = false;
+  std::string input = "triu", dtype = "f64", method = "block", report_dir = ".";
+  for (int i = 2; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+    if (a == "--m") m = std::atoi(next());
+    else if (a == "--input") input = next();
+    else if (a == "--seed") seed = (unsigned)std::strtoul(next(), nullptr, 10);
+    else if (a == "--dtype") dtype = next();
+    else if (a == "--method") method = next();
+    else if (a == "--block") W = std::atoi(next());
+    else if (a == "--max-sweeps") max_sweeps = std::atoi(next());
+    else if (a == "--tol") tol = std::atof(next());
+    else if (a == "--verify") verify = true;
+    else if (a == "--report-dir") report_dir = next();
+    else if (a == "--no-report") report_dir.clear();
+  }
+  if (m < n) {
+    std::fprintf(stderr, "m >= n required\n");
+    return 1;
+  }
+  std::printf("%s\n", svdj_hip_version());
+  std::printf("Dimensions, height: %d, width: %d\n", m, n);
+  std::vector<double> A((size_t)m * n, 0.0);
+  if (input == "dense")
+    svdj_ref_dense_input(m, n, A.data(), m, seed);
+  else
+    svdj_ref_triu_input(m, n, A.data(), m, seed);
+  if (dtype == "f32") return run<float>(m, n, A, method, W, max_sweeps, tol, verify, report_dir);
+  return run<double>(m, n, A, method, W, max_sweeps, tol, verify, report_dir);
+}

@@ -50,7 +50,9 @@ int svdj_tournament(int P, int32_t* held, int32_t* xslot, int32_t* send_to, int3
 
 // ------------------------------------------------------------------ oracle
 // jobu/jobv: 0 = AllVec, 1 = SomeVec, 2 = NoVec (reference SVD_OPTIONS).
-// ordering : 0 = Sameh (reference), 1 = round-robin.
+// ordering : bits 0-3: 0 = Sameh (reference), 1 = round-robin;
+//            bits 4-7: rotation formula 0 = symmetric Schur (reference
+//            main.cu:712-725), 1 = ordered (reference lib/Utils.cu:57-80).
 // tol_mode : 0 = relative |a_p.a_q| > tol*||a_p||*||a_q|| (default),
 //            1 = absolute |a_p.a_q| > tol (reference TOLERANCE=1e-16).
 // Column-major A (m x n, lda) is overwritten by U; s[min(m,n)] gets sigma

@@ -39,7 +39,9 @@ class OracleJacobi(Solver):
         P = C.POINTER(ctype)
         with Timer("cpu") as tm:
             sweeps = fn(int(jobu), int(jobv), m, n, a.ctypes.data_as(P), m, s.ctypes.data_as(P),
-                        v.ctypes.data_as(P), n, 0 if cfg.ordering == "sameh" else 1,
+                        v.ctypes.data_as(P), n,
+                        (0 if cfg.ordering == "sameh" else 1)
+                        | ((1 if cfg.rotation == "ordered" else 0) << 4),
                         cfg.max_sweeps, tol, 1 if cfg.tol_mode == "absolute" else 0,
                         hist.ctypes.data_as(C.POINTER(C.c_double)), cfg.num_threads)
         if sweeps < 0:

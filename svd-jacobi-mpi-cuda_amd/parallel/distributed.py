@@ -35,7 +35,9 @@ from ..config import SolverConfig, SVDOptions
 from ..models.base import SVDResult, Solver
 from ..models.block import choose_block
 from ..ops import kernels as K
+from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
+from ..utils.tracing import trace_range
 from .comm import Communicator
 from .schedule import distributed_sweep_plan, tournament
 
@@ -106,43 +108,39 @@ class DistributedBlockJacobi(Solver):
 
         hist, t_comm, t_total = [], 0.0, 0.0
         sweeps = 0
+        start = 0
+        sig = {"m": m, "n": n, "dtype": str(dtype), "P": P, "W": W, "B": B, "rank": g,
+               "want_v": want_v}
+        if cfg.checkpoint_dir:
+            st = ckpt.load(cfg.checkpoint_dir, g, dev)
+            if st is not None and ckpt.compatible(st, sig):
+                At.copy_(st["At"])
+                D.copy_(st["D"])
+                if want_v:
+                    Vt.copy_(st["Vt"])
+                phys = [list(x) for x in st["phys"]]
+                held = phys[g]
+                hist = list(st["hist"])
+                start = sweeps = int(st["sweep"])
         sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         sync()
         t0 = time.perf_counter()
         converged = False
-        for sw in range(cfg.max_sweeps):
-            K.reset_metric(metric)
-            for r in range(tour.rounds):
-                if r > 0 and P > 1:
-                    tc = time.perf_counter()
-                    x = int(tour.xslot[r, g])
-                    dst, src = int(tour.send_to[r, g]), int(tour.recv_from[r, g])
-                    sl = slice(x * B, (x + 1) * B)
-                    sends = [(At[sl], dst), (D[sl], dst)]
-                    recvs = [(rA, src), (rD, src)]
-                    if want_v:
-                        sends.append((Vt[sl], dst))
-                        recvs.append((rV, src))
-                    comm.sendrecv(sends, recvs)
-                    At[sl].copy_(rA)
-                    D[sl].copy_(rD)
-                    if want_v:
-                        Vt[sl].copy_(rV)
-                    old = [[phys[h][0], phys[h][1]] for h in range(P)]
-                    for h in range(P):
-                        src_h = int(tour.recv_from[r, h])
-                        phys[h][int(tour.xslot[r, h])] = old[src_h][int(tour.xslot[r, src_h])]
-                    held = phys[g]
-                    t_comm += time.perf_counter() - tc
-                plan = plans[r]
-                K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plan.modes, tol,
-                              cfg.max_inner_sweeps, metric)
-            if dev.type == "cuda":
-                pair = K.metric_as_float_pair(metric)
-                mx, nrot = comm.allreduce_max_sum(pair[0], pair[1])
-            else:
-                lmx, lrot = K.read_metric(metric)
-                mx, nrot = comm.allreduce_max_sum(lmx, lrot)
+        bufs = (rA, rV, rD)
+        for sw in range(start, cfg.max_sweeps):
+            with trace_range(f"svdj.sweep{sw}"):
+                K.reset_metric(metric)
+                for r in range(tour.rounds):
+                    if r > 0 and P > 1:
+                        tc = time.perf_counter()
+                        with trace_range("svdj.exchange"):
+                            self._exchange(tour, r, phys, At, Vt, D, bufs, B)
+                        held = phys[g]
+                        t_comm += time.perf_counter() - tc
+                    with trace_range(f"svdj.round{r}"):
+                        K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
+                                      cfg.max_inner_sweeps, metric)
+                mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
             if nrot == 0:
@@ -151,6 +149,12 @@ class DistributedBlockJacobi(Solver):
             # The next sweep replays the same exchange pattern from the current
             # placement: the schedule only depends on positions, so every
             # physical pair still meets exactly once per sweep.
+            if cfg.checkpoint_dir and cfg.checkpoint_every and sweeps % cfg.checkpoint_every == 0:
+                ckpt.save(cfg.checkpoint_dir, g,
+                          {**sig, "At": At, "Vt": Vt if want_v else torch.empty(0), "D": D,
+                           "phys": phys, "hist": hist, "sweep": sweeps})
+        if converged and cfg.checkpoint_dir:
+            ckpt.clear(cfg.checkpoint_dir, g)
         sigma_loc = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         sync()
         t_total = time.perf_counter() - t0
@@ -164,6 +168,40 @@ class DistributedBlockJacobi(Solver):
         return SVDResult(U, S, V, sweeps, hist, t_total, self.name, info)
 
     # ------------------------------------------------------- data movement
+    def _exchange(self, tour, r, phys, At, Vt, D, bufs, B):
+        """Round r of the tournament: this GPU sends the super-block in slot
+        xslot[r][g] (A columns, V columns, squared norms) to send_to[r][g] and
+        receives its replacement from recv_from[r][g] -- one grouped RCCL
+        send/recv.  ``phys`` (every GPU's placement) is updated in place."""
+        g, P = self.comm.rank, self.comm.world
+        rA, rV, rD = bufs
+        x = int(tour.xslot[r, g])
+        dst, src = int(tour.send_to[r, g]), int(tour.recv_from[r, g])
+        sl = slice(x * B, (x + 1) * B)
+        sends = [(At[sl], dst), (D[sl], dst)]
+        recvs = [(rA, src), (rD, src)]
+        if Vt is not None:
+            sends.append((Vt[sl], dst))
+            recvs.append((rV, src))
+        self.comm.sendrecv(sends, recvs)
+        At[sl].copy_(rA)
+        D[sl].copy_(rD)
+        if Vt is not None:
+            Vt[sl].copy_(rV)
+        old = [[phys[h][0], phys[h][1]] for h in range(P)]
+        for h in range(P):
+            src_h = int(tour.recv_from[r, h])
+            phys[h][int(tour.xslot[r, h])] = old[src_h][int(tour.xslot[r, src_h])]
+
+    def _reduce_metric(self, metric, dev):
+        """Global (max off value, total rotations) of the sweep: one all-reduce
+        pair instead of the reference's discarded convergence value."""
+        if dev.type == "cuda":
+            pair = K.metric_as_float_pair(metric)
+            return self.comm.allreduce_max_sum(pair[0], pair[1])
+        lmx, lrot = K.read_metric(metric)
+        return self.comm.allreduce_max_sum(lmx, lrot)
+
     def _distribute(self, A, generator, At, held, m, n, B, dtype):
         comm = self.comm
         if generator is not None:

@@ -99,3 +99,16 @@ def test_cpu_verification_helpers_match_torch():
     rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V)
     assert abs(r - rep["residual_fro"]) < 1e-12
     assert abs(o - rep["orth_u_fro"]) < 1e-12
+
+
+def test_oracle_ordered_rotation_sorts_sigma():
+    """Ordered (Erricos) rotation from reference lib/Utils.cu:57-80: converges to
+    the same SVD and leaves sigma (nearly) sorted in column order."""
+    A = svdj.utils.inputs.random_dense(120, 96, seed=13)
+    res = svdj.svd(A, method="oracle", rotation="ordered", ordering="round_robin")
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert res.converged and rep["residual_rel"] < 1e-12 and rep["sigma_max_rel_err"] < 1e-10
+    inversions = int((res.S[:-1] < res.S[1:]).sum())
+    plain = svdj.svd(A, method="oracle", ordering="round_robin")
+    inv_plain = int((plain.S[:-1] < plain.S[1:]).sum())
+    assert inversions < inv_plain
