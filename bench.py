@@ -43,6 +43,7 @@ def main():
     p.add_argument("--block", type=int, default=None)
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
+    p.add_argument("--chains", type=int, default=2)
     p.add_argument("--json-out", default=None)
     a = p.parse_args()
 
@@ -60,7 +61,7 @@ def main():
     n = a.n
     m = a.m or n
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
-                            max_inner_sweeps=a.inner)
+                            max_inner_sweeps=a.inner, chains=a.chains)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
 

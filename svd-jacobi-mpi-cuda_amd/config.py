@@ -54,6 +54,7 @@ class SolverConfig:
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
     use_graph: bool = False
+    chains: int = 2                 # block path: independent step chains on separate streams
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)

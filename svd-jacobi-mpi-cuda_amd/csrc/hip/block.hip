@@ -456,6 +456,10 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
 }
 
+}  // namespace svdj
+#include "evd2.hpp"
+namespace svdj {
+
 // ------------------------------------------------------------------ apply
 template <typename T, int W>
 __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
@@ -657,8 +661,17 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
                          st, A, lda, m_pad, pr, g.grows, slabs);
     SVDJ_LAUNCH_CHECK();
     if (overlap && s >= 2) SVDJ_HIP_CHECK(hipStreamWaitEvent(st, ss->ev_v[b], 0));
-    hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full, slabs,
-                       g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
+    // The two-level EVD (evd2.hpp) measured 173 vs 152 us per step at
+    // n=4096, W=32 on MI355X (single-wave sub-steps are latency-bound at one
+    // wave per SIMD): opt-in only, kept for further work.
+#ifdef SVDJ_EVD2
+    if constexpr (W == 32)
+      hipLaunchKernelGGL((evd2_kernel<T>), dim3(P), dim3(kEvd2Threads), 0, st, pr, full, slabs,
+                         g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
+    else
+#endif
+      hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full,
+                         slabs, g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     if (overlap) {
       SVDJ_HIP_CHECK(hipEventRecord(ss->ev_q[b], st));

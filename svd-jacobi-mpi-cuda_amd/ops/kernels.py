@@ -162,9 +162,10 @@ def scalar_solve(At, Vt, m_pad, sched, tol, tol_mode, max_sweeps):
 _WS_CACHE: dict = {}
 
 
-def block_workspace(dtype, W, P, m_pad, device) -> torch.Tensor:
+def block_workspace(dtype, W, P, m_pad, device, slot: int = 0) -> torch.Tensor:
+    """Per (device, shape, slot) workspace; concurrent chains use distinct slots."""
     nbytes = int(hip_lib().svdj_block_workspace_bytes(dtype_code(dtype), W, P, m_pad))
-    key = (torch.device(device), dtype, W, P, m_pad)
+    key = (torch.device(device), dtype, W, P, m_pad, slot)
     ws = _WS_CACHE.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -178,16 +179,18 @@ def check_block(dtype, W):
                          f"{SUPPORTED_BLOCK.get(dtype, ())}")
 
 
-def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric):
-    """Run ``len(modes)`` block steps.  pairs: int32 (steps, P, 2) on At's
-    device (block indices local to At); modes: list of 0 (cross) / 1 (full)."""
+def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0):
+    """Run ``len(modes)`` block steps on the current stream.  pairs: int32
+    (steps, P, 2) on At's device (block indices local to At); modes: list of
+    0 (cross) / 1 (full).  Chains running concurrently on different streams
+    must use different ``ws_slot`` values."""
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
     steps, P = int(pairs.shape[0]), int(pairs.shape[1])
     if steps == 0 or P == 0:
         return
     if At.is_cuda:
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device)
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, ws_slot)
         md = (C.c_int32 * steps)(*[int(x) for x in modes])
         n_v = Vt.shape[1] if Vt is not None else 0
         ldv = Vt.stride(0) if Vt is not None else 0

@@ -39,7 +39,7 @@ from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
 from ..utils.tracing import trace_range
 from .comm import Communicator
-from .schedule import distributed_sweep_plan, tournament
+from .schedule import chained_sweep_plan, distributed_sweep_plan, tournament
 
 
 class DistributedBlockJacobi(Solver):
@@ -85,6 +85,12 @@ class DistributedBlockJacobi(Solver):
         tour = tournament(P)
         plans = distributed_sweep_plan(P, k)
         dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
+        chained = chained_sweep_plan(P, k) if cfg.chains >= 2 else None
+        if chained is not None:
+            chained = [[[(torch.from_numpy(c.pairs).to(dev), c.modes) for c in phase]
+                        for phase in rnd] for rnd in chained]
+        streams = (self._chain_streams(dev)
+                   if (chained is not None and dev.type == "cuda") else None)
 
         # ---- resident state: slot s holds super-block held[s]
         # phys[h][s] = super-block physically resident in slot s of GPU h; every
@@ -138,8 +144,12 @@ class DistributedBlockJacobi(Solver):
                         held = phys[g]
                         t_comm += time.perf_counter() - tc
                     with trace_range(f"svdj.round{r}"):
-                        K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                      cfg.max_inner_sweeps, metric)
+                        if chained is None:
+                            K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
+                                          cfg.max_inner_sweeps, metric)
+                        else:
+                            self._run_chained(chained[r], streams, At, Vt, D, m_pad, W, tol,
+                                              metric)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
@@ -166,6 +176,42 @@ class DistributedBlockJacobi(Solver):
         U, S, V = self._gather(At, Vt, sigma_loc, held, m, n, B, dtype, want_v,
                                jobu != SVDOptions.NoVec)
         return SVDResult(U, S, V, sweeps, hist, t_total, self.name, info)
+
+    def _chain_streams(self, dev):
+        """The chain streams are created ONCE per solver and reused: torch
+        hands out pool streams round robin, and HIP binds each new stream to
+        one of GPU_MAX_HW_QUEUES (4) hardware queues, so fresh streams per
+        solve can land on the same queue as each other and serialise."""
+        key = str(dev)
+        cache = self.__dict__.setdefault("_streams", {})
+        if key not in cache:
+            cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
+        return cache[key]
+
+    def _run_chained(self, phases, streams, At, Vt, D, m_pad, W, tol, metric):
+        """Run a round as phases of independent chains.  On the GPU each chain
+        gets its own HIP stream, so the latency-bound EVD of one chain
+        overlaps the bandwidth-bound Gram/apply of the other; phases are
+        joined because consecutive phases share blocks."""
+        inner = self.config.max_inner_sweeps
+        for phase in phases:
+            if streams is None:
+                for c, (pairs, modes) in enumerate(phase):
+                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c)
+                continue
+            main = torch.cuda.current_stream(At.device)
+            # ONE event for all chains: recording a fresh event on the legacy
+            # default stream per chain would make chain c+1 wait for chain c
+            # (null-stream implicit synchronisation) and serialise the phase.
+            ready = torch.cuda.Event()
+            ready.record(main)
+            for c, (pairs, modes) in enumerate(phase):
+                s = streams[c]
+                s.wait_event(ready)
+                with torch.cuda.stream(s):
+                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c)
+            for s in streams[:len(phase)]:
+                main.wait_stream(s)
 
     # ------------------------------------------------------- data movement
     def _exchange(self, tour, r, phys, At, Vt, D, bufs, B):
