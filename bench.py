@@ -44,6 +44,8 @@ def main():
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
     p.add_argument("--chains", type=int, default=2)
+    p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
+                   help="block apply matrix cores (auto: fp32 -> bf16x6 split, fp32-accurate)")
     p.add_argument("--json-out", default=None)
     a = p.parse_args()
 
@@ -61,7 +63,7 @@ def main():
     n = a.n
     m = a.m or n
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
-                            max_inner_sweeps=a.inner, chains=a.chains)
+                            max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
 
@@ -109,6 +111,7 @@ def main():
                 "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                 "block_W": geo["W"],
                 "super_block_B": geo["B"],
+                "mma": a.mma,
             },
             "sweeps": sweeps,
             "converged": conv,

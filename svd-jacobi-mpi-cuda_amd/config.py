@@ -53,7 +53,7 @@ class SolverConfig:
     ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
-    use_graph: bool = False
+    mma: str = "auto"               # block apply matrix cores: auto | native | bf16x6 | bf16x3
     chains: int = 2                 # block path: independent step chains on separate streams
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     checkpoint_dir: str | None = None
@@ -81,7 +81,7 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--max-inner-sweeps", type=int, default=1)
     p.add_argument("--ordering", default="sameh", choices=["sameh", "round_robin"])
     p.add_argument("--sort", action="store_true")
-    p.add_argument("--graph", action="store_true")
+    p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"])
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     return p
@@ -91,5 +91,5 @@ def config_from_args(a) -> SolverConfig:
     return SolverConfig(method=a.method, dtype=_DTYPES[a.dtype] if a.dtype else None,
                         block=a.block, tol=a.tol, tol_mode=a.tol_mode, max_sweeps=a.max_sweeps,
                         max_inner_sweeps=a.max_inner_sweeps, ordering=a.ordering, sort=a.sort,
-                        use_graph=a.graph, checkpoint_dir=a.checkpoint_dir,
+                        mma=a.mma, checkpoint_dir=a.checkpoint_dir,
                         checkpoint_every=a.checkpoint_every)

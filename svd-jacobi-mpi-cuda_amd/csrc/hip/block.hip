@@ -67,10 +67,22 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
     colp[ct] = A + (size_t)col * lda + M::lane_kg(lane) * LPL;
   }
 
-  for (int r0 = r_begin + wave * 32; r0 < r_end; r0 += WAVES * 32) {
-    T v[NCT][LPL];
+  // Software pipeline: the next 32-row slab's loads are issued before this
+  // slab's MFMAs, so HBM latency overlaps matrix-core work (without it the
+  // kernel ran at ~2 TB/s, latency-bound, measured on MI355X at n=16384).
+  int r0 = r_begin + wave * 32;
+  T v[NCT][LPL];
+  if (r0 < r_end) {
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) load_col64B<T>(colp[ct] + r0, v[ct]);
+  }
+  for (; r0 < r_end; r0 += WAVES * 32) {
+    const int rn = r0 + WAVES * 32;
+    T vn[NCT][LPL];
+    if (rn < r_end) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) load_col64B<T>(colp[ct] + rn, vn[ct]);
+    }
 #pragma unroll
     for (int t = 0; t < LPL; ++t) {
       int idx = 0;
@@ -91,6 +103,12 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
             ++idx;
           }
       }
+    }
+    if (rn < r_end) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int t = 0; t < LPL; ++t) v[ct][t] = vn[ct][t];
     }
   }
 
@@ -552,6 +570,146 @@ __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
   }
 }
 
+// -------------------------------------------------- apply on bf16 matrix cores
+// fp32 data, bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate):
+// every operand is split into NP round-to-nearest bf16 parts,
+//   x = x0 + x1 + x2,  |x - x0| <= 2^-9|x|, |x - x0 - x1| <= 2^-18|x|, ...
+// and the products of total order < NP are accumulated in fp32 (bf16 x bf16
+// products are exact):  NP = 3 -> 6 MFMAs (00 01 10 02 11 20), dropped terms
+// are O(2^-26)|x||q|, i.e. fp32 rounding level;  NP = 2 -> 3 MFMAs, O(2^-18)
+// (the "bf16x3" fast mode).  The 2W x 2W Q is split once per workgroup into
+// LDS, already in A-operand fragment order (one ds_read_b128 per part);
+// the X tile is split in registers right after its loads land.
+// Same transposed formulation as apply_kernel: Out^T = Q^T X^T, lane = row.
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+
+template <int NP>
+__device__ __forceinline__ void split_bf16(float x, __bf16 (&p)[NP]) {
+  float r = x;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    p[i] = (__bf16)r;
+    r -= (float)p[i];
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&q)[NP], const bf16x8 (&x)[NP],
+                                             f32x16 acc) {
+  // small terms first
+#pragma unroll
+  for (int ord = NP - 1; ord >= 0; --ord)
+#pragma unroll
+    for (int a = 0; a <= ord; ++a)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[a], x[ord - a], acc, 0, 0, 0);
+  return acc;
+}
+
+template <int W, int NP>
+__global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
+    float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
+    int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
+    const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
+  constexpr int N = 2 * W;
+  constexpr int NCT = N / 32;  // output column tiles
+  constexpr int NKB = N / 16;  // 16-deep k blocks
+  constexpr int WAVES = kApplyThreads / SVDJ_WAVE;
+  static_assert(W % 16 == 0, "k blocks must not straddle the two column blocks");
+  __shared__ bf16x8 Qf[NP][NCT][NKB][SVDJ_WAVE];
+
+  const int pair = blockIdx.x;
+  if (skip[pair]) return;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  int chunk = blockIdx.y;
+  float* base;
+  int ld, r_begin, r_end;
+  if (chunk < a_chunks) {
+    base = A;
+    ld = lda;
+    r_begin = chunk * rows_a;
+    r_end = min(m_pad, r_begin + rows_a);
+  } else {
+    chunk -= a_chunks;
+    base = V;
+    ld = ldv;
+    r_begin = chunk * rows_v;
+    r_end = min(n_v, r_begin + rows_v);
+  }
+  // Q (row-major N x N, fp32) -> split A-operand fragments:
+  // fragment (ct, kb, lane l) = Q[kb*16 + 8(l>>5) + e][ct*32 + (l&31)], e = 0..7
+  const float* Qg = Qall + (size_t)pair * N * N;
+  for (int f = threadIdx.x; f < NCT * NKB * SVDJ_WAVE; f += kApplyThreads) {
+    const int l = f & 63, kb = (f >> 6) % NKB, ct = (f >> 6) / NKB;
+    const int j = ct * 32 + (l & 31), k0 = kb * 16 + 8 * (l >> 5);
+    bf16x8 parts[NP];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 p[NP];
+      split_bf16<NP>(Qg[(k0 + e) * N + j], p);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Qf[i][ct][kb][l] = parts[i];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  float* const xi = base + (size_t)bi * W * ld;
+  float* const xj = base + (size_t)bj * W * ld;
+  // lane part of every address: column offset 8h, row c
+  const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
+  const uint32_t st_off = (uint32_t)(4 * h * ld + c);
+  auto load_tile = [&](float (&x)[NKB][8], int r) {
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      const float* src = kb * 16 < W ? xi + (size_t)(kb * 16) * ld : xj + (size_t)(kb * 16 - W) * ld;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[kb][e] = src[(size_t)e * ld + (lane_off + (uint32_t)r)];
+    }
+  };
+  int r0 = r_begin + wave * 32;
+  if (r0 >= r_end) return;
+  float xr[NKB][8];
+  load_tile(xr, r0);
+  while (true) {
+    const int rn = r0 + WAVES * 32;
+    const bool more = rn < r_end;
+    bf16x8 xs[NKB][NP];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 p[NP];
+        split_bf16<NP>(xr[kb][e], p);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) xs[kb][i][e] = p[i];
+      }
+    if (more) load_tile(xr, rn);  // next tile in flight during this tile's MFMAs
+    // Re-read the Q fragments from LDS per row tile: hoisted out of the loop
+    // they take 96-384 registers (W = 32/64) and force one wave per SIMD.
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      f32x16 acc = Mfma<float>::zero();
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        bf16x8 q[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) q[i] = Qf[i][ct][kb][lane];
+        acc = mfma_split<NP>(q, xs[kb], acc);
+      }
+      float* dst = ct * 32 < W ? xi + (size_t)(ct * 32) * ld : xj + (size_t)(ct * 32 - W) * ld;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        dst[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = acc[e];
+    }
+    if (!more) break;
+    r0 = rn;
+  }
+}
+
 // ------------------------------------------------------------- host side
 struct Geometry {
   int gchunks, grows;  // gram
@@ -588,42 +746,28 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   return ((slabs + 255) / 256 * 256) + 2 * ((q + 255) / 256 * 256) + 2 * ((sk + 255) / 256 * 256);
 }
 
-// Side stream + events for the deferred V update (one set per device).
-struct SideStream {
-  hipStream_t sv = nullptr;
-  hipEvent_t ev_q[2] = {nullptr, nullptr};
-  hipEvent_t ev_v[2] = {nullptr, nullptr};
-};
-static SideStream* side_stream() {
-  static thread_local SideStream cache[16];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  SideStream& s = cache[dev];
-  if (s.sv == nullptr) {
-    if (hipStreamCreateWithFlags(&s.sv, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    for (int i = 0; i < 2; ++i) {
-      if (hipEventCreateWithFlags(&s.ev_q[i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s.ev_v[i], hipEventDisableTiming) != hipSuccess)
-        return nullptr;
-    }
-  }
-  return &s;
-}
-
-// Step pipeline.  Main stream: gram(s) -> evd(s) -> apply_A(s).  The V
-// update of step s only feeds the final result, so it runs on a side stream
-// (waiting for evd(s)) and overlaps gram/evd/apply_A of step s+1; Q and the
-// skip flags are double-buffered, and evd(s+2) waits for apply_V(s) before
-// reusing its buffer.  The caller's stream joins the side stream at the end.
+// Step pipeline on the caller's stream: gram(s) -> evd(s) -> apply(s).
+// Concurrency comes from the caller running independent chains on separate
+// streams (parallel/distributed.py); each chain owns its own workspace.
+// Q and the skip flags are double-buffered so evd(s+1) never overwrites what
+// apply(s) may still read if a caller splits the step across streams.
+//
+// mma: 0 = native matrix cores for the data type (f32 / f64 MFMA),
+//      1 = fp32 data on bf16 MFMA, 3-way split (fp32-level accuracy),
+//      2 = fp32 data on bf16 MFMA, 2-way split (~2^-17 accuracy, fast mode).
 template <typename T, int W>
 static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
                          const int32_t* pairs, int P, int steps, const int32_t* modes,
                          double tol, int max_inner, void* ws, size_t ws_bytes,
-                         uint32_t* metric, hipStream_t st) {
+                         uint32_t* metric, int mma, hipStream_t st) {
   const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad);
   if (ws_bytes < need) {
     set_error("workspace too small: %zu < %zu", ws_bytes, need);
     return -4;
+  }
+  if (mma != 0 && sizeof(T) != 4) {
+    set_error("split-bf16 matrix-core modes need fp32 data");
+    return -3;
   }
   Geometry g = make_geometry(P, m_pad, V ? n_v : 0);
   char* w = (char*)ws;
@@ -634,19 +778,7 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
   w += 2 * qstride;
   const size_t kstride = ((size_t)P * sizeof(int32_t) + 255) / 256 * 256;
   int32_t* skipb[2] = {(int32_t*)w, (int32_t*)(w + kstride)};
-#ifdef SVDJ_V_OVERLAP
-  SideStream* ss = V ? side_stream() : nullptr;
-#else
-  SideStream* ss = nullptr;
-#endif
-  // Measured on MI355X (n=4096, W=32): the side-stream V update does not
-  // overlap usefully with the latency-bound EVD (152 vs 160 us/step), so it
-  // is opt-in (-DSVDJ_V_OVERLAP) until the EVD is restructured.
-#ifdef SVDJ_V_OVERLAP
-  const bool overlap = ss != nullptr && steps > 1;
-#else
-  const bool overlap = false;
-#endif
+  const dim3 apply_grid(P, g.a_chunks + g.v_chunks);
   for (int s = 0; s < steps; ++s) {
     const int b = s & 1;
     T* Q = Qb[b];
@@ -660,11 +792,8 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
       hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(P, g.gchunks), dim3(kGramThreads), 0,
                          st, A, lda, m_pad, pr, g.grows, slabs);
     SVDJ_LAUNCH_CHECK();
-    if (overlap && s >= 2) SVDJ_HIP_CHECK(hipStreamWaitEvent(st, ss->ev_v[b], 0));
-    // The two-level EVD (evd2.hpp) measured 173 vs 152 us per step at
-    // n=4096, W=32 on MI355X (single-wave sub-steps are latency-bound at one
-    // wave per SIMD): opt-in only, kept for further work.
-#ifdef SVDJ_EVD2
+#if defined(SVDJ_EVD2)
+    // Two-level EVD (evd2.hpp): measured slower on MI355X, kept opt-in.
     if constexpr (W == 32)
       hipLaunchKernelGGL((evd2_kernel<T>), dim3(P), dim3(kEvd2Threads), 0, st, pr, full, slabs,
                          g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
@@ -673,25 +802,26 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
       hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full,
                          slabs, g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
-    if (overlap) {
-      SVDJ_HIP_CHECK(hipEventRecord(ss->ev_q[b], st));
-      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks), dim3(kApplyThreads), 0, st,
-                         A, lda, g.a_chunks, g.rows_a, m_pad, (T*)nullptr, ldv, g.rows_v, 0, pr,
-                         Q, skip);
-      SVDJ_LAUNCH_CHECK();
-      SVDJ_HIP_CHECK(hipStreamWaitEvent(ss->sv, ss->ev_q[b], 0));
-      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.v_chunks), dim3(kApplyThreads), 0, ss->sv,
-                         V, ldv, 0, g.rows_a, m_pad, V, ldv, g.rows_v, n_v, pr, Q, skip);
-      SVDJ_LAUNCH_CHECK();
-      SVDJ_HIP_CHECK(hipEventRecord(ss->ev_v[b], ss->sv));
-    } else {
-      hipLaunchKernelGGL((apply_kernel<T, W>), dim3(P, g.a_chunks + g.v_chunks),
-                         dim3(kApplyThreads), 0, st, A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv,
-                         g.rows_v, V ? n_v : 0, pr, Q, skip);
-      SVDJ_LAUNCH_CHECK();
+    if constexpr (sizeof(T) == 4) {
+      if (mma == 1) {
+        hipLaunchKernelGGL((apply_split_kernel<W, 3>), apply_grid, dim3(kApplyThreads), 0, st,
+                           A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0,
+                           pr, Q, skip);
+        SVDJ_LAUNCH_CHECK();
+        continue;
+      }
+      if (mma == 2) {
+        hipLaunchKernelGGL((apply_split_kernel<W, 2>), apply_grid, dim3(kApplyThreads), 0, st,
+                           A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0,
+                           pr, Q, skip);
+        SVDJ_LAUNCH_CHECK();
+        continue;
+      }
     }
+    hipLaunchKernelGGL((apply_kernel<T, W>), apply_grid, dim3(kApplyThreads), 0, st, A, lda,
+                       g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0, pr, Q, skip);
+    SVDJ_LAUNCH_CHECK();
   }
-  if (overlap) SVDJ_HIP_CHECK(hipStreamWaitEvent(st, ss->ev_v[(steps - 1) & 1], 0));
   return 0;
 }
 
@@ -706,7 +836,7 @@ extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad)
 extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                 int ldv, void* D, const int32_t* pairs, int P, int steps,
                                 const int32_t* modes, double tol, int max_inner, void* ws,
-                                size_t ws_bytes, uint32_t* metric, void* stream) {
+                                size_t ws_bytes, uint32_t* metric, int mma, void* stream) {
   if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad) {
     set_error("bad m_pad/lda %d/%d", m_pad, lda);
     return -2;
@@ -715,18 +845,22 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
     set_error("bad n_v/ldv %d/%d", n_v, ldv);
     return -2;
   }
+  if (mma < 0 || mma > 2) {
+    set_error("bad matrix-core mode %d", mma);
+    return -2;
+  }
   if (P <= 0 || steps < 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0 && W == 32)
     return block_steps_t<float, 32>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
-                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, st);
+                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, mma, st);
   if (dtype == 0 && W == 64)
     return block_steps_t<float, 64>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
-                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, st);
+                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, mma, st);
   if (dtype == 1 && W == 32)
     return block_steps_t<double, 32>(m_pad, (double*)A, lda, (double*)V, n_v, ldv, (double*)D,
                                      pairs, P, steps, modes, tol, max_inner, ws, ws_bytes,
-                                     metric, st);
+                                     metric, mma, st);
   set_error("unsupported (dtype=%d, W=%d); supported: fp32 W in {32,64}, fp64 W=32", dtype, W);
   return -3;
 }
@@ -734,8 +868,7 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                 int ldv, void* D, int ncols, double tol, int max_inner,
                                 int max_sweeps, void* ws, size_t ws_bytes, uint32_t* metric,
-                                double* hist, int use_graph, void* stream) {
-  (void)use_graph;
+                                double* hist, int mma, void* stream) {
   if (W <= 0 || ncols % W) {
     set_error("ncols %d not a multiple of W %d", ncols, W);
     return -2;
@@ -769,7 +902,7 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   for (int sw = 0; sw < max_sweeps; ++sw) {
     if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
     rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,
-                          modes.data(), tol, max_inner, ws, ws_bytes, metric, stream);
+                          modes.data(), tol, max_inner, ws, ws_bytes, metric, mma, stream);
     if (rc) break;
     if (hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {

@@ -60,13 +60,16 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   pairs   device int32 [steps][P][2] block indices
 //   modes   host   int32 [steps] (0 cross / 1 full), NULL = all cross
 //   metric  device uint32[2] as for the scalar path.
+//   mma     matrix-core mode: 0 native (f32 / f64 MFMA), 1 fp32 data on bf16
+//           MFMA with a 3-way bf16 split (6 products, fp32-level accuracy),
+//           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
 // Workspace size for one step: svdj_block_workspace_bytes().
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
 int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, const int32_t* pairs, int P,
                      int steps, const int32_t* modes, double tol,
                      int max_inner_sweeps, void* workspace, size_t ws_bytes,
-                     uint32_t* metric, void* stream);
+                     uint32_t* metric, int mma, void* stream);
 
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode.  Returns sweeps, <0 on error.
@@ -74,7 +77,7 @@ int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, int ncols, double tol,
                      int max_inner_sweeps, int max_sweeps, void* workspace,
                      size_t ws_bytes, uint32_t* metric, double* hist,
-                     int use_graph, void* stream);
+                     int mma, void* stream);
 
 // ---------------------------------------------------------------------------
 // Post-processing / utilities.

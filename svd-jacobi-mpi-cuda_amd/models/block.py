@@ -48,11 +48,12 @@ class BlockJacobi(Solver):
         with Timer(device) as tm:
             D = K.col_norms2(At, m_pad)
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
-                                         cfg.max_sweeps, use_graph=cfg.use_graph)
+                                         cfg.max_sweeps, mma=cfg.mma)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:n, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:n, :n].t() if want_v else None
         conv = sweeps < cfg.max_sweeps or (hist and hist[-1] <= tol)
         return SVDResult(U, S[:n], V, sweeps, hist, tm.seconds, self.name,
                          {"tol": tol, "converged": bool(conv), "dtype": str(dtype), "block": W,
+                          "mma": cfg.mma,
                           "device": str(device)})

@@ -22,6 +22,21 @@ from ._native import NativeError, hip_check, hip_lib
 
 ROW_ALIGN = 128
 SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32,)}
+# Matrix-core modes of the block apply (csrc/hip/block.hip): native f32/f64
+# MFMA, or fp32 data on bf16 MFMA with a 3-way (fp32-accurate) / 2-way split.
+MMA_CODES = {"native": 0, "bf16x6": 1, "bf16x3": 2}
+
+
+def mma_code(mma: str | int, dtype: torch.dtype) -> int:
+    if isinstance(mma, int):
+        return mma
+    if mma == "auto":
+        mma = "bf16x6" if dtype == torch.float32 else "native"
+    if mma not in MMA_CODES:
+        raise ValueError(f"bad mma mode {mma!r}; one of {sorted(MMA_CODES)} or 'auto'")
+    if mma != "native" and dtype != torch.float32:
+        raise ValueError(f"mma={mma} needs fp32 data")
+    return MMA_CODES[mma]
 
 
 def dtype_code(dtype: torch.dtype) -> int:
@@ -179,7 +194,8 @@ def check_block(dtype, W):
                          f"{SUPPORTED_BLOCK.get(dtype, ())}")
 
 
-def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0):
+def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0,
+                mma="native"):
     """Run ``len(modes)`` block steps on the current stream.  pairs: int32
     (steps, P, 2) on At's device (block indices local to At); modes: list of
     0 (cross) / 1 (full).  Chains running concurrently on different streams
@@ -197,7 +213,7 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
         hip_check(hip_lib().svdj_block_steps(
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
             _ptr(D), _ptr(pairs), P, steps, md, float(tol), int(max_inner), _ptr(ws),
-            ws.numel(), _ptr(metric), _stream(At)), "block_steps")
+            ws.numel(), _ptr(metric), mma_code(mma, At.dtype), _stream(At)), "block_steps")
     else:
         for s in range(steps):
             mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, bool(modes[s]), tol,
@@ -206,7 +222,7 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             metric[1] += nrot
 
 
-def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, use_graph=False):
+def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
     """Single-device block Jacobi (round-robin over ncols/W blocks, first
     step of each sweep full).  Returns (sweeps, hist)."""
     _check_layout(At, m_pad)
@@ -222,7 +238,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, use_graph=False
         sweeps = hip_check(hip_lib().svdj_block_solve(
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
             ncols, float(tol), int(max_inner), int(max_sweeps), _ptr(ws), ws.numel(),
-            _ptr(metric), hist, int(use_graph), _stream(At)), "block_solve")
+            _ptr(metric), hist, mma_code(mma, At.dtype), _stream(At)), "block_solve")
         return sweeps, [hist[i] for i in range(sweeps)]
     from ..parallel.schedule import round_robin
 
@@ -243,5 +259,5 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, use_graph=False
 __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "dtype_code", "new_metric", "reset_metric",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
-    "block_workspace", "block_steps", "block_solve", "check_block",
+    "block_workspace", "block_steps", "block_solve", "check_block", "MMA_CODES", "mma_code",
 ]

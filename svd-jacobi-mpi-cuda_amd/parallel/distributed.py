@@ -146,7 +146,7 @@ class DistributedBlockJacobi(Solver):
                     with trace_range(f"svdj.round{r}"):
                         if chained is None:
                             K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                          cfg.max_inner_sweeps, metric)
+                                          cfg.max_inner_sweeps, metric, mma=cfg.mma)
                         else:
                             self._run_chained(chained[r], streams, At, Vt, D, m_pad, W, tol,
                                               metric)
@@ -197,7 +197,8 @@ class DistributedBlockJacobi(Solver):
         for phase in phases:
             if streams is None:
                 for c, (pairs, modes) in enumerate(phase):
-                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c)
+                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
+                                  mma=self.config.mma)
                 continue
             main = torch.cuda.current_stream(At.device)
             # ONE event for all chains: recording a fresh event on the legacy
@@ -209,7 +210,8 @@ class DistributedBlockJacobi(Solver):
                 s = streams[c]
                 s.wait_event(ready)
                 with torch.cuda.stream(s):
-                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c)
+                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
+                                  mma=self.config.mma)
             for s in streams[:len(phase)]:
                 main.wait_stream(s)
 

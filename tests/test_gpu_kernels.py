@@ -58,9 +58,11 @@ def test_scalar_step_matches_reference(svdj, cuda, dtype):
     torch.testing.assert_close(Vt.double().cpu(), Vt_ref, rtol=tol_cmp, atol=tol_cmp)
 
 
-@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64), (torch.float64, 32)])
+@pytest.mark.parametrize("dtype,W,mma", [(torch.float32, 32, "native"), (torch.float32, 64, "native"),
+                                         (torch.float64, 32, "native"), (torch.float32, 32, "bf16x6"),
+                                         (torch.float32, 64, "bf16x6")])
 @pytest.mark.parametrize("full", [1, 0])
-def test_block_step_matches_reference(svdj, cuda, dtype, W, full):
+def test_block_step_matches_reference(svdj, cuda, dtype, W, mma, full):
     """One gram -> evd -> apply step vs the fp64 torch reference on the same input."""
     K = svdj.ops.kernels
     R = svdj.ops.reference
@@ -82,7 +84,7 @@ def test_block_step_matches_reference(svdj, cuda, dtype, W, full):
     At64, Vt64, D64 = At.double().cpu(), Vt.double().cpu(), D.double().cpu()
     tol = 1e-6 if dtype == torch.float32 else 1e-13
     metric = K.new_metric(cuda)
-    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [full], tol, 12, metric)
+    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [full], tol, 12, metric, mma=mma)
     mx_ref, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, bool(full), tol, 12)
     mx, nrot = K.read_metric(metric)
     assert nrot == nrot_ref == 2
@@ -113,12 +115,15 @@ def test_block_step_matches_reference(svdj, cuda, dtype, W, full):
                                rtol=0, atol=vtol)
 
 
-@pytest.mark.parametrize("method,dtype", [("block", torch.float32), ("block", torch.float64),
-                                          ("scalar", torch.float32), ("scalar", torch.float64)])
-def test_svd_end_to_end(svdj, cuda, method, dtype):
+@pytest.mark.parametrize("method,dtype,mma", [("block", torch.float32, "native"),
+                                              ("block", torch.float32, "bf16x6"),
+                                              ("block", torch.float64, "native"),
+                                              ("scalar", torch.float32, "native"),
+                                              ("scalar", torch.float64, "native")])
+def test_svd_end_to_end(svdj, cuda, method, dtype, mma):
     m, n = 520, 384
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=3)
-    res = svdj.svd(A.to(cuda), method=method, dtype=dtype)
+    res = svdj.svd(A.to(cuda), method=method, dtype=dtype, mma=mma)
     assert res.converged, res.history
     rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
     eps = torch.finfo(dtype).eps
@@ -140,3 +145,46 @@ def test_gesvd_inplace_reference_signature(svdj, cuda):
     rep = svdj.utils.metrics.verify(A, U, s, Vm, torch.linalg.svdvals(A.cpu()))
     assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-9, rep
     assert res.sweeps >= 2
+
+
+def test_block_bf16x3_fast_mode(svdj, cuda):
+    """2-way bf16 split: ~2^-17 accurate products, so the relative threshold
+    is set at that level; residual and orthogonality follow it."""
+    m, n = 600, 512
+    A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=8)
+    res = svdj.svd(A.to(cuda), method="block", dtype=torch.float32, mma="bf16x3", tol=2e-5)
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-4 and rep["sigma_max_abs_err_over_smax"] < 1e-4, rep
+    assert rep["orth_v_fro"] < 1e-2, rep
+
+
+@pytest.mark.parametrize("W", [32, 64])
+def test_bf16x6_matches_native(svdj, cuda, W):
+    """bf16x6 apply is as accurate as the f32 MFMA apply.  One step from the
+    same input (same Gram and Q in both modes) agrees to fp32 rounding level;
+    after a whole sweep (rotation sequences may legitimately diverge) V is
+    as orthogonal as with the native apply."""
+    K = svdj.ops.kernels
+    n = 8 * W
+    A = svdj.utils.inputs.random_dense(n, n, dtype=torch.float32, device=cuda, seed=11)
+    pairs = torch.from_numpy(svdj.parallel.schedule.round_robin(n // W)).to(cuda)
+    eye = torch.eye(n, dtype=torch.float64)
+    step, orth = [], []
+    for mma in ("native", "bf16x6"):
+        for nsteps in (1, n // W - 1):
+            At = A.t().contiguous()
+            Vt = torch.zeros(n, n, dtype=torch.float32, device=cuda)
+            K.set_identity(Vt, n)
+            D = K.col_norms2(At, n)
+            K.block_steps(At, Vt, D, n, pairs[:nsteps], W, [1] + [0] * (nsteps - 1), 1e-6, 1,
+                          K.new_metric(cuda), mma=mma)
+            v = Vt.double().cpu()
+            if nsteps == 1:
+                step.append((At.double().cpu(), v))
+            else:
+                orth.append(float((v @ v.t() - eye).abs().max()))
+    (a0, v0), (a1, v1) = step
+    assert (a0 - a1).abs().max() / a0.abs().max() < 2e-6
+    assert (v0 - v1).abs().max() < 2e-6
+    assert orth[1] < 4 * orth[0] + 1e-6, orth

@@ -20,6 +20,7 @@ p.add_argument("--block", type=int, default=32)
 p.add_argument("--dtype", default="fp32")
 p.add_argument("--inner", default="0,1,2")
 p.add_argument("--reps", type=int, default=3)
+p.add_argument("--mma", default="native")
 a = p.parse_args()
 K = svdj.ops.kernels
 dt = torch.float32 if a.dtype == "fp32" else torch.float64
@@ -40,10 +41,11 @@ for inner in [int(x) for x in a.inner.split(",")]:
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        K.block_steps(At, Vt, D, n, pairs, W, modes, 1e-30 if inner > 0 else 1e30, inner, metric)
+        K.block_steps(At, Vt, D, n, pairs, W, modes, 1e-30 if inner > 0 else 1e30, inner, metric,
+                      mma=a.mma)
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     per_step = min(times) / (nb - 1) * 1e3
-    print(json.dumps({"n": n, "W": W, "dtype": a.dtype, "inner": inner, "sweep_ms": round(min(times), 3),
+    print(json.dumps({"n": n, "W": W, "dtype": a.dtype, "inner": inner, "mma": a.mma, "sweep_ms": round(min(times), 3),
                       "us_per_step": round(per_step, 2)}), flush=True)
