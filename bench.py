@@ -32,6 +32,41 @@ BASELINE_METRIC = ("GFLOP/s + time-to-converge (sweeps to ||off||<tol), N×N den
                    "1/2/4/8 MI355X")
 
 
+def verify_distributed(res, gen, m, n, comm, dtype):
+    """Accuracy of the (distributed) result, after the timed region.
+
+    Every rank regenerates A (same seeded generator) and checks its own
+    columns: ||A V_loc - U_loc S_loc||_F^2 and ||[U_loc|V_loc]^T[..] - I||_F^2,
+    summed over ranks (fp32 GEMMs, accurate to ~1e-6 relative).  Padding
+    columns (global index >= n) are excluded."""
+    geo = res.info["geometry"]
+    B = geo["B"]
+    held = res.info["held"]
+    A = torch.cat([gen(c0, min(c0 + B, n)) for c0 in range(0, n, B)], dim=1).to(dtype)
+    At, Vt, S = res.U, res.V, res.S
+    cols = []
+    for s, sb in enumerate(held):
+        for j in range(B):
+            if sb * B + j < n:
+                cols.append(s * B + j)
+    idx = torch.tensor(cols, device=At.device, dtype=torch.long)
+    U = At[idx, :m].t()
+    V = Vt[idx, :n].t()
+    sig = S[idx]
+    R = A @ V - U * sig
+    eye = torch.eye(len(cols), device=At.device, dtype=dtype)
+    parts = torch.stack([R.double().pow(2).sum(), A.double().pow(2).sum() / comm.world,
+                         (V.t() @ V - eye).double().pow(2).sum(),
+                         (U.t() @ U - eye).double().pow(2).sum()])
+    if comm.distributed:
+        import torch.distributed as dist
+        dist.all_reduce(parts)
+    parts = parts.cpu()
+    return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
+            "orth_v_blockdiag_fro": float(parts[2].sqrt()),
+            "orth_u_blockdiag_fro": float(parts[3].sqrt())}
+
+
 def main():
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument("--gpus", type=int, default=1)
@@ -45,8 +80,11 @@ def main():
     p.add_argument("--inner", type=int, default=1)
     p.add_argument("--chains", type=int, default=2)
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
-                   help="block apply matrix cores (auto: fp32 -> bf16x6 split, fp32-accurate)")
+                   help="block apply matrix cores (auto = native f32/f64 MFMA; bf16x6/bf16x3 "
+                        "split modes are faster but not fp32-accurate on every input)")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the post-timing accuracy check")
     a = p.parse_args()
 
     import svdj
@@ -90,6 +128,7 @@ def main():
     gflops = flops / elapsed / 1e9
     ms = elapsed / a.steps * 1e3
     geo = results[-1].info["geometry"]
+    acc = None if a.no_verify else verify_distributed(results[-1], gen, m, n, comm, dtype)
     if comm.rank == 0:
         line = {
             "metric": BASELINE_METRIC,
@@ -118,6 +157,7 @@ def main():
             "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % h) for h in results[-1].history[-3:]],
             "comm_seconds_rank0": round(results[-1].info["comm_seconds"], 4),
+            "accuracy": acc,
         }
         print(json.dumps(line), flush=True)
         if a.json_out:

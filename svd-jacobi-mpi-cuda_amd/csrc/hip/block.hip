@@ -582,28 +582,43 @@ __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
 // the X tile is split in registers right after its loads land.
 // Same transposed formulation as apply_kernel: Out^T = Q^T X^T, lane = row.
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+#ifndef SVDJ_SPLIT_INT
+#define SVDJ_SPLIT_INT 0
+#endif
 
 template <int NP>
 __device__ __forceinline__ void split_bf16(float x, __bf16 (&p)[NP]) {
   float r = x;
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
+#if SVDJ_SPLIT_INT
+    // explicit round-to-nearest-even to 8 significant bits
+    uint32_t u = __float_as_uint(r);
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    const float hi = __uint_as_float(u);
+    p[i] = __builtin_bit_cast(__bf16, (unsigned short)(u >> 16));
+    r -= hi;
+#else
     p[i] = (__bf16)r;
     r -= (float)p[i];
+#endif
   }
 }
 
-template <int NP>
+// Products of total order >= LO (small terms first).
+template <int NP, int LO>
 __device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&q)[NP], const bf16x8 (&x)[NP],
                                              f32x16 acc) {
-  // small terms first
 #pragma unroll
-  for (int ord = NP - 1; ord >= 0; --ord)
+  for (int ord = NP - 1; ord >= LO; --ord)
 #pragma unroll
     for (int a = 0; a <= ord; ++a)
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[a], x[ord - a], acc, 0, 0, 0);
   return acc;
 }
+#ifndef SVDJ_SPLIT_ACC
+#define SVDJ_SPLIT_ACC 1
+#endif
 
 template <int W, int NP>
 __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
@@ -692,14 +707,25 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      f32x16 acc = Mfma<float>::zero();
+      f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
         bf16x8 q[NP];
 #pragma unroll
         for (int i = 0; i < NP; ++i) q[i] = Qf[i][ct][kb][lane];
-        acc = mfma_split<NP>(q, xs[kb], acc);
+        if constexpr (SVDJ_SPLIT_ACC == 0) {
+          acc = mfma_split<NP, 0>(q, xs[kb], acc);
+        } else {
+          lo = mfma_split<NP, 1>(q, xs[kb], lo);
+          if constexpr (SVDJ_SPLIT_ACC == 1) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], acc, 0, 0, 0);
+          } else {
+            acc += __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], Mfma<float>::zero(),
+                                                           0, 0, 0);
+          }
+        }
       }
+      if constexpr (SVDJ_SPLIT_ACC != 0) acc += lo;
       float* dst = ct * 32 < W ? xi + (size_t)(ct * 32) * ld : xj + (size_t)(ct * 32 - W) * ld;
 #pragma unroll
       for (int e = 0; e < 16; ++e)
@@ -755,6 +781,11 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
 // mma: 0 = native matrix cores for the data type (f32 / f64 MFMA),
 //      1 = fp32 data on bf16 MFMA, 3-way split (fp32-level accuracy),
 //      2 = fp32 data on bf16 MFMA, 2-way split (~2^-17 accuracy, fast mode).
+// Measured (tools/probe_apply.py, bench.py accuracy check): the split modes
+// are as accurate as f32 MFMA on unstructured data, but the bf16 MFMA's
+// internal accumulation is biased when one 16-product group mixes magnitudes
+// (a dominant column, or Q ~ I late in the iteration): on U(0,1) 8192^2 the
+// final ||AV - US||/||A|| is 6.5e-4 vs 8e-6 native.  Native is the default.
 template <typename T, int W>
 static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
                          const int32_t* pairs, int P, int steps, const int32_t* modes,
@@ -918,4 +949,60 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   }
   (void)hipFreeAsync(dpairs, st);
   return rc ? rc : sweeps;
+}
+
+// Test/diagnostic hook: X <- X Q for ONE column-block pair (blocks 0 and 1 of
+// X, 2W columns with leading dimension ld, rows padded to SVDJ_ROW_ALIGN),
+// Q row-major 2W x 2W on the device, with the given matrix-core mode.
+extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q,
+                            void* stream) {
+  if (rows <= 0 || rows % SVDJ_ROW_ALIGN || ld < rows) {
+    set_error("bad rows/ld %d/%d", rows, ld);
+    return -2;
+  }
+  static const int32_t hpair[2] = {0, 1};
+  static const int32_t hskip[1] = {0};
+  hipStream_t st = (hipStream_t)stream;
+  int32_t* dbuf = nullptr;
+  SVDJ_HIP_CHECK(hipMallocAsync((void**)&dbuf, 3 * sizeof(int32_t), st));
+  SVDJ_HIP_CHECK(hipMemcpyAsync(dbuf, hpair, 2 * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  SVDJ_HIP_CHECK(hipMemcpyAsync(dbuf + 2, hskip, sizeof(int32_t), hipMemcpyHostToDevice, st));
+  const int rows_chunk = 512, chunks = (rows + rows_chunk - 1) / rows_chunk;
+  const dim3 grid(1, chunks), blk(kApplyThreads);
+  int rc = 0;
+  if (dtype == 0 && mma == 1 && W == 64)
+    hipLaunchKernelGGL((apply_split_kernel<64, 3>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 0 && mma == 1 && W == 32)
+    hipLaunchKernelGGL((apply_split_kernel<32, 3>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 0 && mma == 2 && W == 64)
+    hipLaunchKernelGGL((apply_split_kernel<64, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 0 && mma == 2 && W == 32)
+    hipLaunchKernelGGL((apply_split_kernel<32, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 0 && mma == 0 && W == 64)
+    hipLaunchKernelGGL((apply_kernel<float, 64>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 0 && mma == 0 && W == 32)
+    hipLaunchKernelGGL((apply_kernel<float, 32>), grid, blk, 0, st, (float*)X, ld, chunks,
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  else if (dtype == 1 && mma == 0 && W == 32)
+    hipLaunchKernelGGL((apply_kernel<double, 32>), grid, blk, 0, st, (double*)X, ld, chunks,
+                       rows_chunk, rows, (double*)nullptr, 0, 0, 0, dbuf, (const double*)Q,
+                       dbuf + 2);
+  else {
+    set_error("svdj_apply_q: unsupported dtype=%d W=%d mma=%d", dtype, W, mma);
+    rc = -3;
+  }
+  if (rc == 0) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      set_error("svdj_apply_q launch: %s", hipGetErrorString(e));
+      rc = -101;
+    }
+  }
+  (void)hipFreeAsync(dbuf, st);
+  return rc;
 }

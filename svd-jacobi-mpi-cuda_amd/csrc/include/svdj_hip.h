@@ -79,6 +79,11 @@ int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      size_t ws_bytes, uint32_t* metric, double* hist,
                      int mma, void* stream);
 
+// Diagnostic hook: X <- X Q for one pair of column blocks (X = 2W columns,
+// leading dimension ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major
+// 2W x 2W on the device, with matrix-core mode `mma` (as svdj_block_steps).
+int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q, void* stream);
+
 // ---------------------------------------------------------------------------
 // Post-processing / utilities.
 // V := I on an (n_v x ncols) column-major block (rows >= ncols zeroed).

@@ -113,6 +113,8 @@ def hip_lib():
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int, c_void_p])
+        _sig(lib, "svdj_apply_q", c_int,
+             [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,
              [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
         _sig(lib, "svdj_col_norms2", c_int, [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p])

@@ -23,7 +23,10 @@ from ._native import NativeError, hip_check, hip_lib
 ROW_ALIGN = 128
 SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32,)}
 # Matrix-core modes of the block apply (csrc/hip/block.hip): native f32/f64
-# MFMA, or fp32 data on bf16 MFMA with a 3-way (fp32-accurate) / 2-way split.
+# MFMA (default, fp32-exact products and sums), or fp32 data on bf16 MFMA
+# with a 3-way / 2-way operand split -- faster (memory-bound instead of
+# MFMA-bound at W=64) but NOT fp32-accurate on every input: the bf16 MFMA's
+# internal accumulation is biased when magnitudes mix (see block.hip).
 MMA_CODES = {"native": 0, "bf16x6": 1, "bf16x3": 2}
 
 
@@ -31,7 +34,7 @@ def mma_code(mma: str | int, dtype: torch.dtype) -> int:
     if isinstance(mma, int):
         return mma
     if mma == "auto":
-        mma = "bf16x6" if dtype == torch.float32 else "native"
+        mma = "native"
     if mma not in MMA_CODES:
         raise ValueError(f"bad mma mode {mma!r}; one of {sorted(MMA_CODES)} or 'auto'")
     if mma != "native" and dtype != torch.float32:
@@ -222,6 +225,16 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             metric[1] += nrot
 
 
+def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
+    """Xt (2W, ld) rows = columns of X, in place X <- X Q (device tensors)."""
+    _check_layout(Xt, Xt.shape[1] // ROW_ALIGN * ROW_ALIGN)
+    if Xt.shape[0] != 2 * W or tuple(Q.shape) != (2 * W, 2 * W) or not Q.is_contiguous():
+        raise ValueError("Xt must be (2W, ld) and Q contiguous (2W, 2W)")
+    rows = Xt.shape[1] // ROW_ALIGN * ROW_ALIGN
+    hip_check(hip_lib().svdj_apply_q(dtype_code(Xt.dtype), W, mma_code(mma, Xt.dtype), _ptr(Xt),
+                                     rows, Xt.stride(0), _ptr(Q), _stream(Xt)), "apply_q")
+
+
 def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
     """Single-device block Jacobi (round-robin over ncols/W blocks, first
     step of each sweep full).  Returns (sweeps, hist)."""
@@ -260,4 +273,5 @@ __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "dtype_code", "new_metric", "reset_metric",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_solve", "check_block", "MMA_CODES", "mma_code",
+    "apply_q",
 ]
