@@ -74,7 +74,9 @@ def main():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--n", type=int, default=16384)
     p.add_argument("--m", type=int, default=None)
-    p.add_argument("--dtype", default="fp32", choices=["fp32", "fp64"])
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "fp64", "bf16"])
+    p.add_argument("--precondition", default="auto", choices=["none", "qr", "auto"],
+                   help="QR-precondition tall inputs (m >= 2n); flops then count QR + GEMM")
     p.add_argument("--block", type=int, default=None)
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
@@ -97,17 +99,19 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     comm = Communicator()
-    dtype = torch.float32 if a.dtype == "fp32" else torch.float64
+    dtype = {"fp32": torch.float32, "fp64": torch.float64, "bf16": torch.bfloat16}[a.dtype]
+    work = torch.float64 if dtype == torch.float64 else torch.float32
     n = a.n
     m = a.m or n
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
-                            max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma)
+                            max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
+                            precondition=a.precondition)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
 
     def gen(c0, c1):  # synthetic random dense U(0,1), column-block seeded
         g = torch.Generator(device=dev).manual_seed(1234 + c0)
-        return torch.rand(m, c1 - c0, generator=g, dtype=dtype, device=dev)
+        return torch.rand(m, c1 - c0, generator=g, dtype=work, device=dev).to(dtype)
 
     def one():
         return solver.solve(None, m=m, n=n, dtype=dtype, generator=gen, gather=False)
@@ -124,11 +128,11 @@ def main():
 
     sweeps = [r.sweeps for r in results]
     conv = all(r.converged for r in results)
-    flops = sum(svdj.utils.metrics.algorithmic_flops_per_sweep(m, n) * s for s in sweeps)
+    flops = sum(r.info["flops"] for r in results)
     gflops = flops / elapsed / 1e9
     ms = elapsed / a.steps * 1e3
     geo = results[-1].info["geometry"]
-    acc = None if a.no_verify else verify_distributed(results[-1], gen, m, n, comm, dtype)
+    acc = None if a.no_verify else verify_distributed(results[-1], gen, m, n, comm, work)
     if comm.rank == 0:
         line = {
             "metric": BASELINE_METRIC,
@@ -150,7 +154,8 @@ def main():
                 "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                 "block_W": geo["W"],
                 "super_block_B": geo["B"],
-                "mma": a.mma,
+                "mma": results[-1].info.get("mma", a.mma),
+                "precondition": results[-1].info.get("precondition", "none"),
             },
             "sweeps": sweeps,
             "converged": conv,

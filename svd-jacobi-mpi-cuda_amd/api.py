@@ -15,6 +15,7 @@ import torch
 from .config import SolverConfig, SVDOptions
 from .models.base import SVDResult, sort_result
 from .models.block import BlockJacobi
+from .models import precondition as pre
 from .models.oracle import OracleJacobi
 from .models.scalar import ScalarJacobi
 
@@ -51,10 +52,21 @@ def svd(A: torch.Tensor, jobu=SVDOptions.AllVec, jobv=SVDOptions.AllVec,
         jobu, jobv = jobv, jobu
     method = _pick_method(cfg, dev, A.shape[1])
     solver = _METHODS[method](cfg)
+    mm, nn = A.shape
+    Q = None
+    if pre.use_qr(cfg, mm, nn):
+        # tall-skinny: Jacobi on R (n x n), U = Q U_R (models/precondition.py)
+        Q, R = pre.qr(A.to(dev), cfg.resolved_dtype(A))
+        A = R.to(A.dtype) if cfg.bf16_mode(A) else R
     if method == "oracle":
         res = solver.solve(A, jobu, jobv)
     else:
         res = solver.solve(A, jobu, jobv, device=dev)
+    if Q is not None:
+        if res.U is not None:
+            res.U = (Q.to(res.U.device) @ res.U.to(Q.dtype)).to(res.U.dtype)
+        res.info["precondition"] = "qr"
+    res.info["flops"] = pre.flops(mm, nn, res.sweeps, Q is not None)
     if transposed:
         res.U, res.V = res.V, res.U
         res.info["transposed"] = True

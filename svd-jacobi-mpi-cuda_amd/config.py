@@ -38,13 +38,13 @@ class SVDOptions(enum.IntEnum):
 
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "fp64": torch.float64,
-           "float64": torch.float64}
+           "float64": torch.float64, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
 
 
 @dataclass
 class SolverConfig:
     method: str = "auto"            # auto | block | scalar | oracle
-    dtype: torch.dtype | None = None  # compute dtype (None: input dtype if fp32/fp64)
+    dtype: torch.dtype | None = None  # fp32 | fp64 | bf16 (None: the input's dtype)
     block: int | None = None        # block width W (block path); None: auto
     tol: float | None = None        # rotation threshold; None: 4 sqrt(m) eps
     tol_mode: str = "relative"      # relative | absolute (reference parity)
@@ -54,16 +54,37 @@ class SolverConfig:
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
     mma: str = "auto"               # block apply matrix cores: auto | native | bf16x6 | bf16x3
+    precondition: str = "auto"      # auto | qr | none  (QR first when m >= qr_ratio * n)
+    qr_ratio: float = 2.0
     chains: int = 2                 # block path: independent step chains on separate streams
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
 
-    def resolved_dtype(self, A: torch.Tensor) -> torch.dtype:
+    def bf16_mode(self, A: torch.Tensor | None = None) -> bool:
+        """bf16 problem: bf16 in/out, fp32 master copies of A and V, block
+        apply on bf16 matrix cores (2-way split) and a bf16-level stop test."""
         if self.dtype is not None:
-            return self.dtype
-        return A.dtype if A.dtype in (torch.float32, torch.float64) else torch.float32
+            return self.dtype == torch.bfloat16
+        return A is not None and A.dtype == torch.bfloat16
+
+    def resolved_dtype(self, A: torch.Tensor | None) -> torch.dtype:
+        """Storage/compute dtype of the working copies (fp32 or fp64)."""
+        if self.dtype is not None:
+            return torch.float32 if self.dtype == torch.bfloat16 else self.dtype
+        if A is not None and A.dtype == torch.float64:
+            return torch.float64
+        return torch.float32
+
+    def precision_dtype(self, A: torch.Tensor | None) -> torch.dtype:
+        """The dtype whose accuracy the stop test targets."""
+        return torch.bfloat16 if self.bf16_mode(A) else self.resolved_dtype(A)
+
+    def resolved_mma(self, A: torch.Tensor | None) -> str:
+        if self.mma != "auto":
+            return self.mma
+        return "bf16x3" if self.bf16_mode(A) else "native"
 
     def to_dict(self) -> dict:
         d = asdict(self)
@@ -82,6 +103,7 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--ordering", default="sameh", choices=["sameh", "round_robin"])
     p.add_argument("--sort", action="store_true")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"])
+    p.add_argument("--precondition", default="auto", choices=["auto", "qr", "none"])
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     return p
@@ -91,5 +113,5 @@ def config_from_args(a) -> SolverConfig:
     return SolverConfig(method=a.method, dtype=_DTYPES[a.dtype] if a.dtype else None,
                         block=a.block, tol=a.tol, tol_mode=a.tol_mode, max_sweeps=a.max_sweeps,
                         max_inner_sweeps=a.max_inner_sweeps, ordering=a.ordering, sort=a.sort,
-                        mma=a.mma, checkpoint_dir=a.checkpoint_dir,
+                        mma=a.mma, precondition=a.precondition, checkpoint_dir=a.checkpoint_dir,
                         checkpoint_every=a.checkpoint_every)

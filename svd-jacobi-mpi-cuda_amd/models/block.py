@@ -32,6 +32,8 @@ class BlockJacobi(Solver):
         jobu, jobv = SVDOptions.parse(jobu), SVDOptions.parse(jobv)
         device = torch.device(device) if device is not None else A.device
         dtype = cfg.resolved_dtype(A)
+        bf16 = cfg.bf16_mode(A)
+        mma = cfg.resolved_mma(A)
         m, n = A.shape
         if m < n:
             raise ValueError("block path expects m >= n (api.svd transposes wide inputs)")
@@ -44,16 +46,19 @@ class BlockJacobi(Solver):
         Vt = torch.zeros(ncols, n_v, dtype=dtype, device=device) if want_v else None
         if want_v:
             K.set_identity(Vt, ncols)
-        tol = self.tolerance(dtype, m)
+        tol = self.tolerance(cfg.precision_dtype(A), m)
         with Timer(device) as tm:
             D = K.col_norms2(At, m_pad)
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
-                                         cfg.max_sweeps, mma=cfg.mma)
+                                         cfg.max_sweeps, mma=mma)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:n, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:n, :n].t() if want_v else None
+        if bf16:  # bf16 in/out; sigma stays fp32
+            U = U.to(torch.bfloat16) if U is not None else None
+            V = V.to(torch.bfloat16) if V is not None else None
         conv = sweeps < cfg.max_sweeps or (hist and hist[-1] <= tol)
         return SVDResult(U, S[:n], V, sweeps, hist, tm.seconds, self.name,
                          {"tol": tol, "converged": bool(conv), "dtype": str(dtype), "block": W,
-                          "mma": cfg.mma,
+                          "mma": mma, "bf16": bf16,
                           "device": str(device)})

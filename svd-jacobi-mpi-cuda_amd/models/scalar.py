@@ -36,13 +36,16 @@ class ScalarJacobi(Solver):
             K.set_identity(Vt, n)
         sched_np = sameh(n) if cfg.ordering == "sameh" else round_robin_padded(n)
         sched = torch.from_numpy(sched_np).to(device)
-        tol = self.tolerance(dtype, m)
+        tol = self.tolerance(cfg.precision_dtype(A), m)
         tol_mode = 1 if cfg.tol_mode == "absolute" else 0
         with Timer(device) as tm:
             sweeps, hist = K.scalar_solve(At, Vt, m_pad, sched, tol, tol_mode, cfg.max_sweeps)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:, :n].t() if want_v else None
+        if cfg.bf16_mode(A):
+            U = U.to(torch.bfloat16) if U is not None else None
+            V = V.to(torch.bfloat16) if V is not None else None
         conv = sweeps < cfg.max_sweeps or (hist and hist[-1] <= tol)
         return SVDResult(U, S, V, sweeps, hist, tm.seconds, self.name,
                          {"tol": tol, "converged": bool(conv), "dtype": str(dtype),

@@ -33,6 +33,7 @@ import torch
 
 from ..config import SolverConfig, SVDOptions
 from ..models.base import SVDResult, Solver
+from ..models import precondition as pre
 from ..models.block import choose_block
 from ..ops import kernels as K
 from ..utils import checkpoint as ckpt
@@ -60,25 +61,78 @@ class DistributedBlockJacobi(Solver):
                 "n_v": pad_rows(ncols)}
 
     # --------------------------------------------------------------- solve
+    _DT_CODE = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}
+
     def solve(self, A: torch.Tensor | None = None, jobu=SVDOptions.AllVec,
               jobv=SVDOptions.AllVec, m: int | None = None, n: int | None = None,
               dtype: torch.dtype | None = None, generator=None, gather: bool = True,
               time_only: bool = False) -> SVDResult:
+        """Distributed SVD.  ``dtype`` is the problem precision (fp32, fp64 or
+        bf16 = bf16 data on fp32 master copies and bf16 matrix cores).  Tall
+        inputs (m >= qr_ratio n, or precondition="qr") are QR-preconditioned:
+        every rank factors the generated A redundantly (no communication), or
+        rank 0 factors its root-owned A; the sweeps then run on R (n x n) and
+        U = Q U_R (models/precondition.py)."""
         comm, cfg = self.comm, self.config
         dev = comm.device
         jobu, jobv = SVDOptions.parse(jobu), SVDOptions.parse(jobv)
         # ---- problem description (root-owned input is broadcast as shape)
         if A is not None:
             m, n = A.shape
-            dtype = dtype or cfg.resolved_dtype(A)
-        hdr = torch.tensor([m or 0, n or 0, 1 if (dtype or torch.float32) == torch.float64 else 0],
-                           dtype=torch.int64, device=dev)
+            dtype = dtype or cfg.dtype or A.dtype
+        dtype = dtype or cfg.dtype or torch.float32
+        if dtype not in self._DT_CODE:
+            dtype = torch.float32
+        hdr = torch.tensor([m or 0, n or 0, self._DT_CODE[dtype]], dtype=torch.int64, device=dev)
         if generator is None and comm.distributed:
             comm.broadcast(hdr, 0)
         m, n = int(hdr[0]), int(hdr[1])
-        dtype = torch.float64 if int(hdr[2]) == 1 else torch.float32
+        dtype = {0: torch.float32, 1: torch.float64, 2: torch.bfloat16}[int(hdr[2])]
         if m < n:
             raise ValueError("distributed path expects m >= n")
+        work = torch.float64 if dtype == torch.float64 else torch.float32
+        if not pre.use_qr(cfg, m, n):
+            res = self._solve(A, jobu, jobv, m, n, dtype, generator, gather, time_only)
+            res.info["flops"] = pre.flops(m, n, res.sweeps, False)
+            return res
+        # ---- QR-preconditioned tall-skinny solve
+        Q = None
+        if generator is not None:
+            Afull = torch.cat([generator(c0, min(c0 + 1024, n)) for c0 in range(0, n, 1024)],
+                              dim=1).to(device=dev, dtype=work)
+            Q, R = pre.qr(Afull, work)
+            del Afull
+            res = self._solve(None, jobu, jobv, n, n, dtype, lambda c0, c1: R[:, c0:c1], gather,
+                              time_only)
+        else:
+            R = None
+            if comm.rank == 0:
+                Q, R = pre.qr(A.to(dev), work)
+            res = self._solve(R, jobu, jobv, n, n, dtype, None, gather, time_only)
+            if comm.distributed and jobu != SVDOptions.NoVec and res.info.get("distributed_output"):
+                if Q is None:
+                    Q = torch.empty(m, n, dtype=work, device=dev)
+                comm.broadcast(Q, 0)
+        if jobu != SVDOptions.NoVec and res.U is not None and Q is not None:
+            if res.info.get("distributed_output"):
+                Ut = res.U  # (2B, pad(n)) transposed local columns of U_R
+                Uloc = Q @ Ut[:, :n].to(work).t()
+                At = torch.zeros(Ut.shape[0], pad_rows(m), dtype=Ut.dtype, device=dev)
+                At[:, :m] = Uloc.t()
+                res.U = At
+                res.info["geometry"] = {**res.info["geometry"], "m_pad": pad_rows(m)}
+            else:
+                res.U = (Q @ res.U.to(work)).to(res.U.dtype)
+        res.info["precondition"] = "qr"
+        res.info["flops"] = pre.flops(m, n, res.sweeps, True)
+        return res
+
+    def _solve(self, A, jobu, jobv, m, n, pdtype, generator, gather, time_only) -> SVDResult:
+        comm, cfg = self.comm, self.config
+        dev = comm.device
+        dtype = torch.float64 if pdtype == torch.float64 else torch.float32
+        bf16 = pdtype == torch.bfloat16
+        mma = cfg.mma if cfg.mma != "auto" else ("bf16x3" if bf16 else "native")
         geo = self.geometry(m, n, dtype)
         P, W, B, k, m_pad, n_v, ncols = (geo[x] for x in ("P", "W", "B", "k", "m_pad", "n_v", "ncols"))
         g = comm.rank
@@ -105,7 +159,7 @@ class DistributedBlockJacobi(Solver):
             for s in range(2):
                 K.set_identity(Vt[s * B:(s + 1) * B], B, held[s] * B)
         D = K.col_norms2(At, m_pad)
-        tol = self.tolerance(dtype, m)
+        tol = self.tolerance(pdtype, m)
         rA = torch.empty(B, m_pad, dtype=dtype, device=dev)
         rV = torch.empty(B, n_v, dtype=dtype, device=dev) if want_v else None
         rD = torch.empty(B, dtype=dtype, device=dev)
@@ -146,10 +200,10 @@ class DistributedBlockJacobi(Solver):
                     with trace_range(f"svdj.round{r}"):
                         if chained is None:
                             K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                          cfg.max_inner_sweeps, metric, mma=cfg.mma)
+                                          cfg.max_inner_sweeps, metric, mma=mma)
                         else:
                             self._run_chained(chained[r], streams, At, Vt, D, m_pad, W, tol,
-                                              metric)
+                                              metric, mma)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
@@ -168,13 +222,16 @@ class DistributedBlockJacobi(Solver):
         sigma_loc = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         sync()
         t_total = time.perf_counter() - t0
-        info = {"tol": tol, "converged": converged, "dtype": str(dtype), "geometry": geo,
+        info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
         if time_only or not gather:
             return SVDResult(At if jobu != SVDOptions.NoVec else None, sigma_loc, Vt, sweeps, hist,
                              t_total, self.name, {**info, "distributed_output": True})
         U, S, V = self._gather(At, Vt, sigma_loc, held, m, n, B, dtype, want_v,
                                jobu != SVDOptions.NoVec)
+        if bf16:  # bf16 in/out (sigma stays fp32)
+            U = U.to(torch.bfloat16) if U is not None else None
+            V = V.to(torch.bfloat16) if V is not None else None
         return SVDResult(U, S, V, sweeps, hist, t_total, self.name, info)
 
     def _chain_streams(self, dev):
@@ -188,7 +245,7 @@ class DistributedBlockJacobi(Solver):
             cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
         return cache[key]
 
-    def _run_chained(self, phases, streams, At, Vt, D, m_pad, W, tol, metric):
+    def _run_chained(self, phases, streams, At, Vt, D, m_pad, W, tol, metric, mma="native"):
         """Run a round as phases of independent chains.  On the GPU each chain
         gets its own HIP stream, so the latency-bound EVD of one chain
         overlaps the bandwidth-bound Gram/apply of the other; phases are
@@ -198,7 +255,7 @@ class DistributedBlockJacobi(Solver):
             if streams is None:
                 for c, (pairs, modes) in enumerate(phase):
                     K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
-                                  mma=self.config.mma)
+                                  mma=mma)
                 continue
             main = torch.cuda.current_stream(At.device)
             # ONE event for all chains: recording a fresh event on the legacy
@@ -211,7 +268,7 @@ class DistributedBlockJacobi(Solver):
                 s.wait_event(ready)
                 with torch.cuda.stream(s):
                     K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
-                                  mma=self.config.mma)
+                                  mma=mma)
             for s in streams[:len(phase)]:
                 main.wait_stream(s)
 

@@ -62,5 +62,8 @@ def verify(A, U, S, V, sigma_ref=None) -> dict:
 
 def default_tol(dtype: torch.dtype, m: int) -> float:
     """Relative rotation threshold: 4 sqrt(m) eps (computed dot products of
-    length m carry ~sqrt(m) eps relative noise; tighter never stops)."""
-    return 4.0 * math.sqrt(max(m, 1)) * torch.finfo(dtype).eps
+    length m carry ~sqrt(m) eps relative noise; tighter never stops).  For
+    bf16 problems eps is that of the 2-way bf16 split arithmetic (2^-17),
+    which is ~2^9 below the bf16 output rounding."""
+    eps = 2.0 ** -17 if dtype == torch.bfloat16 else torch.finfo(dtype).eps
+    return 4.0 * math.sqrt(max(m, 1)) * eps

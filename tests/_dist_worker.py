@@ -14,10 +14,11 @@ def main():
     m, n, W, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     mode = sys.argv[5] if len(sys.argv) > 5 else "root"
     comm = Communicator(backend="gloo", device=torch.device("cpu"))
-    cfg = svdj.SolverConfig(block=W, dtype=torch.float64, max_inner_sweeps=1)
+    cfg = svdj.SolverConfig(block=W, dtype=torch.float64, max_inner_sweeps=1,
+                            precondition="qr" if mode.endswith("qr") else "none")
     solver = DistributedBlockJacobi(cfg, comm)
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=9)
-    if mode == "root":
+    if mode in ("root", "rootqr"):
         res = solver.solve(A if comm.rank == 0 else None)
     else:
         res = solver.solve(None, m=m, n=n, dtype=torch.float64,

@@ -79,3 +79,34 @@ def test_reference_ops_block_step_orthogonalises_pair():
         assert off.abs().max() < 1e-10 * g.diagonal().max()
     torch.testing.assert_close(Vt @ A0, At, atol=1e-12, rtol=0)  # A_new = A_old V (Vt rows = V cols)
     torch.testing.assert_close(D, torch.diagonal(G), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("method", ["oracle", "block"])
+def test_qr_preconditioned_tall_skinny(method):
+    """m >= 2n: A = QR, Jacobi on R, U = Q U_R (models/precondition.py)."""
+    A = svdj.utils.inputs.random_dense(400, 96, seed=12)
+    res = svdj.svd(A, method=method, dtype=torch.float64)
+    assert res.info.get("precondition") == "qr"
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-10, rep
+    assert res.U.shape == (400, 96)
+    plain = svdj.svd(A, method=method, dtype=torch.float64, precondition="none")
+    assert "precondition" not in plain.info
+    # flop accounting: QR + sweeps on n x n + GEMM
+    m, n = A.shape
+    assert res.info["flops"] == svdj.models.precondition.flops(m, n, res.sweeps, True)
+
+
+def test_bf16_mode_cpu():
+    """bf16 problem: bf16 in/out, fp32 working copies, bf16-level stop test."""
+    A = svdj.utils.inputs.random_dense(120, 96, seed=13).to(torch.bfloat16)
+    res = svdj.svd(A, method="block")
+    assert res.U.dtype == torch.bfloat16 and res.V.dtype == torch.bfloat16
+    assert res.S.dtype == torch.float32
+    assert res.info["bf16"] and res.info["mma"] == "bf16x3"
+    ref = torch.linalg.svdvals(A.double())
+    rep = svdj.utils.metrics.verify(A.double(), res.U, res.S, res.V, ref)
+    assert rep["sigma_max_abs_err_over_smax"] < 1e-4, rep
+    assert rep["residual_rel"] < 2e-2, rep  # U, V rounded to bf16
+    cfg = svdj.SolverConfig(dtype=torch.bfloat16)
+    assert cfg.resolved_dtype(None) == torch.float32 and cfg.precision_dtype(None) == torch.bfloat16

@@ -41,3 +41,10 @@ def test_distributed_block_jacobi_gloo(world, m, n, tmp_path):
 def test_distributed_generator_input(tmp_path):
     rep = _run(2, 150, 128, 32, tmp_path, mode="gen")
     assert rep["converged"] and rep["residual_rel"] < 1e-12, rep
+
+
+@pytest.mark.parametrize("mode", ["rootqr", "genqr"])
+def test_distributed_qr_preconditioned(mode, tmp_path):
+    rep = _run(2, 300, 128, 32, tmp_path, mode=mode)
+    assert rep["converged"] and rep["residual_rel"] < 1e-12, rep
+    assert rep["orth_u_fro"] < 1e-10 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep

@@ -70,3 +70,27 @@ def test_checkpoint_resume_gpu(svdj, cuda, tmp_path):
     res = DistributedBlockJacobi(svdj.SolverConfig(block=32, checkpoint_dir=str(tmp_path),
                                                    checkpoint_every=1), comm).solve(A)
     assert res.sweeps == ref.sweeps and torch.equal(res.S, ref.S)
+
+
+def test_tall_skinny_bf16_qr_gpu(svdj, cuda):
+    """Config-4 shape class on one GPU: tall bf16 input, QR preconditioning,
+    fp32 working copies, bf16 matrix cores (bf16x3) for the apply."""
+    A = svdj.utils.inputs.random_dense(2048, 512, dtype=torch.float32, device=cuda,
+                                       seed=14).to(torch.bfloat16)
+    res = svdj.svd(A, method="block")
+    assert res.converged and res.info["precondition"] == "qr" and res.info["mma"] == "bf16x3"
+    assert res.U.dtype == torch.bfloat16 and res.U.shape == (2048, 512)
+    rep = svdj.utils.metrics.verify(A.double(), res.U, res.S, res.V,
+                                    torch.linalg.svdvals(A.double().cpu()))
+    assert rep["sigma_max_abs_err_over_smax"] < 1e-4, rep
+    assert rep["residual_rel"] < 2e-2, rep
+
+
+def test_qr_preconditioned_fp32_gpu(svdj, cuda):
+    A = svdj.utils.inputs.random_dense(3000, 640, dtype=torch.float32, device=cuda, seed=15)
+    res = svdj.svd(A, method="block")
+    plain = svdj.svd(A, method="block", precondition="none")
+    ref = torch.linalg.svdvals(A.double().cpu())
+    for r in (res, plain):
+        rep = svdj.utils.metrics.verify(A, r.U, r.S, r.V, ref)
+        assert r.converged and rep["residual_rel"] < 1e-4 and rep["sigma_max_abs_err_over_smax"] < 1e-5, rep
