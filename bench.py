@@ -72,7 +72,7 @@ def main():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--n", type=int, default=16384)
+    p.add_argument("--n", "--size", dest="n", type=int, default=16384)
     p.add_argument("--m", type=int, default=None)
     p.add_argument("--dtype", default="fp32", choices=["fp32", "fp64", "bf16"])
     p.add_argument("--precondition", default="auto", choices=["none", "qr", "auto"],

@@ -33,10 +33,14 @@ class Communicator:
                  timeout_s: float = 600.0, init: bool = True):
         rank, world, local = env_world()
         if device is None:
-            device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+            # SVDJ_SHARED_GPU=1: every rank on cuda:0 (rehearsing the multi-rank
+            # RCCL path on a one-GPU box; not a performance configuration)
+            idx = 0 if os.environ.get("SVDJ_SHARED_GPU") == "1" else local
+            device = torch.device("cuda", idx) if torch.cuda.is_available() else torch.device("cpu")
         self.device = torch.device(device)
         if backend is None:
-            backend = "nccl" if self.device.type == "cuda" else "gloo"
+            backend = os.environ.get("SVDJ_COMM_BACKEND") or (
+                "nccl" if self.device.type == "cuda" else "gloo")
         self.backend = backend
         self.owns_group = False
         if world > 1 and init and not dist.is_initialized():
@@ -65,6 +69,17 @@ class Communicator:
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+
+    def isendrecv(self, sends: list, recvs: list) -> list:
+        """Like :meth:`sendrecv` but returns the works without waiting: on the
+        GPU the transfer runs on the RCCL stream after the CURRENT stream's
+        prior work, and ``work.wait()`` later makes the waiting stream (not
+        the host) depend on it -- so compute on other streams overlaps it."""
+        if not self.distributed:
+            raise RuntimeError("isendrecv on a single rank")
+        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends if d != self.rank]
+        ops += [dist.P2POp(dist.irecv, t, s) for t, s in recvs if s != self.rank]
+        return dist.batch_isend_irecv(ops) if ops else []
 
     # ---------------------------------------------------------- collectives
     def allreduce_max_sum(self, mx: float | torch.Tensor, cnt: float | torch.Tensor):

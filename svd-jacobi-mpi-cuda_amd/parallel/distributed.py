@@ -40,7 +40,8 @@ from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
 from ..utils.tracing import trace_range
 from .comm import Communicator
-from .schedule import chained_sweep_plan, distributed_sweep_plan, tournament
+from .pipeline import PipelineExecutor, sweep_plan
+from .schedule import distributed_sweep_plan, tournament
 
 
 class DistributedBlockJacobi(Solver):
@@ -55,7 +56,9 @@ class DistributedBlockJacobi(Solver):
         P = self.comm.world
         W = self.config.block or choose_block(dtype, max(n // max(P, 1), 1), m)
         K.check_block(dtype, W)
-        ncols = round_up(max(n, 2 * P * W), 2 * P * W)
+        # pipelined sweeps split super-blocks in halves: k = B/W must be even
+        q = (4 if self.config.chains >= 2 else 2) * P * W
+        ncols = round_up(max(n, q), q)
         B = ncols // (2 * P)
         return {"P": P, "W": W, "ncols": ncols, "B": B, "k": B // W, "m_pad": pad_rows(m),
                 "n_v": pad_rows(ncols)}
@@ -137,14 +140,13 @@ class DistributedBlockJacobi(Solver):
         P, W, B, k, m_pad, n_v, ncols = (geo[x] for x in ("P", "W", "B", "k", "m_pad", "n_v", "ncols"))
         g = comm.rank
         tour = tournament(P)
-        plans = distributed_sweep_plan(P, k)
-        dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
-        chained = chained_sweep_plan(P, k) if cfg.chains >= 2 else None
-        if chained is not None:
-            chained = [[[(torch.from_numpy(c.pairs).to(dev), c.modes) for c in phase]
-                        for phase in rnd] for rnd in chained]
-        streams = (self._chain_streams(dev)
-                   if (chained is not None and dev.type == "cuda") else None)
+        pipelined = cfg.chains >= 2
+        if pipelined:
+            splan = sweep_plan(P, k, tour.xslot[:, g])
+        else:
+            plans = distributed_sweep_plan(P, k)
+            dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
+        streams = self._chain_streams(dev) if (pipelined and dev.type == "cuda") else None
 
         # ---- resident state: slot s holds super-block held[s]
         # phys[h][s] = super-block physically resident in slot s of GPU h; every
@@ -187,10 +189,19 @@ class DistributedBlockJacobi(Solver):
         t0 = time.perf_counter()
         converged = False
         bufs = (rA, rV, rD)
+        if pipelined:
+            ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour)
+
+            def run_steps(pairs, modes, slot):
+                K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
+                              metric, slot, mma=mma)
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
-                for r in range(tour.rounds):
+                if pipelined:
+                    t_comm += ex.run(splan, run_steps, phys)
+                    held = phys[g]
+                for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:
                         tc = time.perf_counter()
                         with trace_range("svdj.exchange"):
@@ -198,12 +209,8 @@ class DistributedBlockJacobi(Solver):
                         held = phys[g]
                         t_comm += time.perf_counter() - tc
                     with trace_range(f"svdj.round{r}"):
-                        if chained is None:
-                            K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                          cfg.max_inner_sweeps, metric, mma=mma)
-                        else:
-                            self._run_chained(chained[r], streams, At, Vt, D, m_pad, W, tol,
-                                              metric, mma)
+                        K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
+                                      cfg.max_inner_sweeps, metric, mma=mma)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
@@ -245,33 +252,6 @@ class DistributedBlockJacobi(Solver):
             cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
         return cache[key]
 
-    def _run_chained(self, phases, streams, At, Vt, D, m_pad, W, tol, metric, mma="native"):
-        """Run a round as phases of independent chains.  On the GPU each chain
-        gets its own HIP stream, so the latency-bound EVD of one chain
-        overlaps the bandwidth-bound Gram/apply of the other; phases are
-        joined because consecutive phases share blocks."""
-        inner = self.config.max_inner_sweeps
-        for phase in phases:
-            if streams is None:
-                for c, (pairs, modes) in enumerate(phase):
-                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
-                                  mma=mma)
-                continue
-            main = torch.cuda.current_stream(At.device)
-            # ONE event for all chains: recording a fresh event on the legacy
-            # default stream per chain would make chain c+1 wait for chain c
-            # (null-stream implicit synchronisation) and serialise the phase.
-            ready = torch.cuda.Event()
-            ready.record(main)
-            for c, (pairs, modes) in enumerate(phase):
-                s = streams[c]
-                s.wait_event(ready)
-                with torch.cuda.stream(s):
-                    K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, inner, metric, c,
-                                  mma=mma)
-            for s in streams[:len(phase)]:
-                main.wait_stream(s)
-
     # ------------------------------------------------------- data movement
     def _exchange(self, tour, r, phys, At, Vt, D, bufs, B):
         """Round r of the tournament: this GPU sends the super-block in slot
@@ -288,7 +268,12 @@ class DistributedBlockJacobi(Solver):
         if Vt is not None:
             sends.append((Vt[sl], dst))
             recvs.append((rV, src))
+        host_sync = At.is_cuda and self.comm.backend != "nccl"  # gloo rehearsal, see pipeline.py
+        if host_sync:
+            torch.cuda.synchronize(At.device)
         self.comm.sendrecv(sends, recvs)
+        if host_sync:
+            torch.cuda.synchronize(At.device)
         At[sl].copy_(rA)
         D[sl].copy_(rD)
         if Vt is not None:

@@ -1,0 +1,288 @@
+"""Half-block pipelined sweep: RCCL exchange overlapped with compute.
+
+The tournament (schedule.tournament) replaces ONE resident super-block per
+GPU between rounds.  Done as a whole (parallel/distributed.py ``_exchange``)
+the exchange sits between rounds with the GPU idle: at n=16384 on 8 GPUs
+that is 15 x 134 MB per sweep per GPU over one xGMI link.  The reference's
+exchange (rank-0 star, host-staged, reference main.cu:582-680, 854-936) is
+fully serial as well.
+
+Here every super-block is handled as two halves and a round's cross work is
+four half-pair tasks (I = incoming slot, S = staying slot):
+
+    stream 0:  T00 = I0 x S0   ->  T01 = I0 x S1
+    stream 1:  T10 = I1 x S0   ->  T11 = I1 x S1
+
+Half 0 of the next outgoing slot is last touched by T01/T10, half 1 by T11,
+so the send/recv of half 0 is issued right after T10 and runs under T11;
+half 1 is issued after T11 and runs under the next round's T00' and T01'
+(which only need the already-arrived half 0).  Every task waits only on the
+events of the tasks that last touched its two halves, so the two compute
+streams and the RCCL stream overlap as far as the data dependencies allow.
+Round 0 of every sweep also runs the within-super-block round robins
+(RR(slot 0) || RR(slot 1)).  Every block pair of the matrix still meets
+exactly once per sweep (checked by tests/test_pipeline_cpu.py).
+
+On CPU tensors (gloo tests) the same item list runs sequentially, with the
+exchanges blocking at their trigger points -- identical arithmetic.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .schedule import round_robin
+
+
+@dataclass
+class Task:
+    """One chain of block steps on local block indices."""
+    name: str
+    pairs: np.ndarray        # (steps, pairs_per_step, 2)
+    modes: list
+    stream: int
+    halves: tuple            # ((slot, half), ...) touched
+
+
+@dataclass
+class Send:
+    """Exchange of half ``half`` of slot ``slot`` before round ``round``."""
+    round: int
+    slot: int
+    half: int
+
+
+@dataclass
+class SweepPlan:
+    P: int
+    k: int
+    items: list = field(default_factory=list)   # Task | Send, in issue order
+
+
+def _blocks(slot: int, half: int, k: int) -> list:
+    h = k // 2
+    return list(range(slot * k + half * h, slot * k + (half + 1) * h))
+
+
+def _bipartite(xs: list, ys: list) -> np.ndarray:
+    h = len(xs)
+    out = np.zeros((h, h, 2), dtype=np.int32)
+    for t in range(h):
+        for a in range(h):
+            out[t, a] = (xs[a], ys[(a + t) % h])
+    return out
+
+
+def sweep_plan(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
+    """Items of one sweep.  ``xslot[r]`` is the slot replaced before round r
+    (r >= 1), as produced by schedule.tournament."""
+    if k < 2 or k % 2:
+        raise ValueError(f"pipelined sweep needs an even block count per super-block, got {k}")
+    plan = SweepPlan(P, k)
+    rr = round_robin(k)
+    rr_modes = [1] + [0] * (k - 2)
+    plan.items.append(Task("rr0", rr.copy(), rr_modes, 0, ((0, 0), (0, 1))))
+    plan.items.append(Task("rr1", rr + k, rr_modes, 1, ((1, 0), (1, 1))))
+    R = 2 * P - 1
+    for r in range(R):
+        inc = int(xslot[r]) if r > 0 else 0
+        stay = 1 - inc
+        h = k // 2
+
+        def task(name, ih, sh, stream):
+            return Task(f"r{r}.{name}", _bipartite(_blocks(inc, ih, k), _blocks(stay, sh, k)),
+                        [0] * h, stream, ((inc, ih), (stay, sh)))
+
+        nxt = int(xslot[r + 1]) if r + 1 < R else None
+        plan.items += [task("T00", 0, 0, 0), task("T01", 0, 1, 0), task("T10", 1, 0, 1)]
+        if nxt is not None:
+            plan.items.append(Send(r + 1, nxt, 0))
+        plan.items.append(task("T11", 1, 1, 1))
+        if nxt is not None:
+            plan.items.append(Send(r + 1, nxt, 1))
+    return plan
+
+
+def check_plan_coverage(plans: list, tour) -> None:
+    """Simulate one sweep on every GPU (``plans[g]`` is GPU g's plan; all have
+    the same item structure) on global block ids, from the tournament's
+    starting placement; assert that every pair of global blocks meets
+    exactly once.  Raises AssertionError."""
+    P = len(plans)
+    k = plans[0].k
+    h = k // 2
+    # place[g][slot][half] = (super-block, half) currently resident
+    place = [[[(int(tour.held[0, g, s]), hh) for hh in range(2)] for s in range(2)]
+             for g in range(P)]
+    met = {}
+    n_items = len(plans[0].items)
+    assert all(len(p.items) == n_items for p in plans)
+    for i in range(n_items):
+        its = [p.items[i] for p in plans]
+        if isinstance(its[0], Send):
+            assert all(isinstance(x, Send) and x.half == its[0].half and x.round == its[0].round
+                       for x in its)
+            r, hh = its[0].round, its[0].half
+            new = [None] * P
+            for g in range(P):
+                src = int(tour.recv_from[r, g])
+                assert int(tour.send_to[r, src]) == g
+                new[g] = place[src][its[src].slot][hh]
+            for g in range(P):
+                place[g][its[g].slot][hh] = new[g]
+            continue
+        for g in range(P):
+            it = its[g]
+            for t in range(it.pairs.shape[0]):
+                for a, b in it.pairs[t]:
+                    ga = _global_block(place[g], int(a), k, h)
+                    gb = _global_block(place[g], int(b), k, h)
+                    assert ga != gb
+                    key = (min(ga, gb), max(ga, gb))
+                    met[key] = met.get(key, 0) + 1
+    nb = 2 * P * k
+    assert len(met) == nb * (nb - 1) // 2, (len(met), nb * (nb - 1) // 2)
+    assert all(v == 1 for v in met.values())
+
+
+def _global_block(place_g, b: int, k: int, h: int) -> int:
+    slot, rem = divmod(b, k)
+    half, off = divmod(rem, h)
+    sb, hh = place_g[slot][half]
+    return sb * k + hh * h + off
+
+
+class PipelineExecutor:
+    """Runs a :class:`SweepPlan` on the resident buffers of one rank."""
+
+    def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour):
+        self.comm, self.streams = comm, streams
+        self.At, self.Vt, self.D = At, Vt, D
+        self.k, self.W, self.tour = k, W, tour
+        self.hB = k // 2 * W
+        dev = At.device
+        self.cuda = dev.type == "cuda"
+        hB = self.hB
+        self.rbuf = [(torch.empty(hB, At.shape[1], dtype=At.dtype, device=dev),
+                      torch.empty(hB, Vt.shape[1], dtype=Vt.dtype, device=dev) if Vt is not None
+                      else None,
+                      torch.empty(hB, dtype=D.dtype, device=dev)) for _ in range(2)]
+        self.dev_pairs = {}  # item index -> device pairs (the plan is fixed per solve)
+        self.comm_stream = torch.cuda.Stream(dev) if self.cuda and comm.distributed else None
+
+    def _rows(self, slot: int, half: int) -> slice:
+        b0 = slot * self.k * self.W + half * self.hB
+        return slice(b0, b0 + self.hB)
+
+    def _pairs(self, i: int, task: Task):
+        t = self.dev_pairs.get(i)
+        if t is None:
+            t = torch.from_numpy(task.pairs).to(self.At.device)
+            self.dev_pairs[i] = t
+        return t
+
+    def run(self, plan: SweepPlan, run_steps, phys) -> float:
+        """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
+        steps on the current stream.  ``phys`` (per-GPU placement of whole
+        super-blocks) is updated after both halves of a round arrived.
+        Returns host seconds spent issuing/blocking on exchanges."""
+        import time
+
+        if self.cuda:  # everything enqueued on the caller's stream so far (metric
+            # reset, initial norms) happens before any task or exchange
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.At.device))
+            for s in self.streams + ([self.comm_stream] if self.comm_stream else []):
+                s.wait_event(ready)
+        last = {}       # (slot, half) -> [events of tasks since last exchange]
+        pending = {}    # (slot, half) -> (works, buffers) received, not yet copied
+        t_comm = 0.0
+        halves_done = {}
+        for i, it in enumerate(plan.items):
+            if isinstance(it, Send):
+                tc = time.perf_counter()
+                self._send(it, last, pending)
+                halves_done[it.round] = halves_done.get(it.round, 0) + 1
+                if halves_done[it.round] == 2:
+                    self._update_phys(it.round, phys)
+                t_comm += time.perf_counter() - tc
+                continue
+            pairs = self._pairs(i, it)
+            if not self.cuda:
+                for hv in it.halves:
+                    self._consume(hv, pending)
+                run_steps(pairs, it.modes, it.stream)
+                continue
+            s = self.streams[it.stream]
+            with torch.cuda.stream(s):
+                for hv in it.halves:
+                    for ev in last.get(hv, ()):
+                        s.wait_event(ev)
+                    self._consume(hv, pending)
+                run_steps(pairs, it.modes, it.stream)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            for hv in it.halves:
+                last.setdefault(hv, []).append(ev)
+        if self.cuda:
+            main = torch.cuda.current_stream(self.At.device)
+            for s in self.streams:
+                main.wait_stream(s)
+        return t_comm
+
+    def _send(self, it: Send, last, pending):
+        comm, tour = self.comm, self.tour
+        g = comm.rank
+        r, x, hh = it.round, it.slot, it.half
+        dst, src = int(tour.send_to[r, g]), int(tour.recv_from[r, g])
+        sl = self._rows(x, hh)
+        rA, rV, rD = self.rbuf[hh]
+        sends = [(self.At[sl], dst), (self.D[sl], dst)]
+        recvs = [(rA, src), (rD, src)]
+        if self.Vt is not None:
+            sends.append((self.Vt[sl], dst))
+            recvs.append((rV, src))
+        if not comm.distributed:
+            raise RuntimeError("exchange on a single rank")
+        if not self.cuda:
+            comm.sendrecv(sends, recvs)
+            self._copy_in(sl, hh)
+            last.pop((x, hh), None)
+            return
+        cs = self.comm_stream
+        for ev in last.pop((x, hh), ()):
+            cs.wait_event(ev)
+        if comm.backend != "nccl":
+            # gloo on device tensors (one-GPU rehearsal of the multi-rank
+            # path) does not order its copies after other streams: make the
+            # data ready on the host side first.  RCCL needs none of this.
+            cs.synchronize()
+        with torch.cuda.stream(cs):
+            works = comm.isendrecv(sends, recvs)
+        pending[(x, hh)] = works
+
+    def _consume(self, hv, pending):
+        works = pending.pop(hv, None)
+        if works is None:
+            return
+        for w in works:
+            w.wait()  # current (consumer) stream waits for send + recv
+        if self.cuda and self.comm.backend != "nccl":
+            torch.cuda.synchronize(self.At.device)
+        self._copy_in(self._rows(*hv), hv[1])
+
+    def _copy_in(self, sl, hh):
+        rA, rV, rD = self.rbuf[hh]
+        self.At[sl].copy_(rA)
+        self.D[sl].copy_(rD)
+        if self.Vt is not None:
+            self.Vt[sl].copy_(rV)
+
+    def _update_phys(self, r: int, phys):
+        tour, P = self.tour, self.comm.world
+        old = [[phys[h][0], phys[h][1]] for h in range(P)]
+        for h in range(P):
+            src_h = int(tour.recv_from[r, h])
+            phys[h][int(tour.xslot[r, h])] = old[src_h][int(tour.xslot[r, src_h])]

@@ -1,0 +1,40 @@
+"""Half-block pipelined sweep plan (parallel/pipeline.py): coverage and
+exchange structure on CPU."""
+import pytest
+
+import svdj
+pipeline = svdj.parallel.pipeline
+schedule = svdj.parallel.schedule
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("k", [2, 4, 6])
+def test_every_block_pair_meets_once(P, k):
+    tour = schedule.tournament(P)
+    plans = [pipeline.sweep_plan(P, k, tour.xslot[:, g]) for g in range(P)]
+    pipeline.check_plan_coverage(plans, tour)
+
+
+def test_sends_follow_last_use():
+    """Half 0 of the next outgoing slot is sent after its last user in the
+    round, and before anything of the next round touches it."""
+    P, k = 4, 4
+    tour = schedule.tournament(P)
+    plan = pipeline.sweep_plan(P, k, tour.xslot[:, 0])
+    items = plan.items
+    for i, it in enumerate(items):
+        if not isinstance(it, pipeline.Send):
+            continue
+        hv = (it.slot, it.half)
+        prev = [j for j in range(i) if isinstance(items[j], pipeline.Task)
+                and hv in items[j].halves and f"r{it.round - 1}." in items[j].name]
+        later = [j for j in range(i + 1, len(items)) if isinstance(items[j], pipeline.Task)
+                 and hv in items[j].halves]
+        assert prev, it
+        assert all(f"r{it.round}." in items[j].name or items[j].name.startswith("r" + str(it.round + 1))
+                   or int(items[j].name[1:].split(".")[0]) > it.round - 1 for j in later[:1])
+
+
+def test_odd_k_rejected():
+    with pytest.raises(ValueError):
+        pipeline.sweep_plan(2, 3, schedule.tournament(2).xslot[:, 0])
