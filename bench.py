@@ -109,9 +109,15 @@ def main():
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
 
-    def gen(c0, c1):  # synthetic random dense U(0,1), column-block seeded
-        g = torch.Generator(device=dev).manual_seed(1234 + c0)
-        return torch.rand(m, c1 - c0, generator=g, dtype=work, device=dev).to(dtype)
+    GB = 256  # generator block: the matrix is fixed regardless of how callers chunk it
+
+    def gen(c0, c1):  # synthetic random dense U(0,1), columns c0..c1-1 of ONE fixed matrix
+        parts = []
+        for b0 in range(c0 // GB * GB, c1, GB):
+            g = torch.Generator(device=dev).manual_seed(1234 + b0)
+            blk = torch.rand(m, GB, generator=g, dtype=work, device=dev)
+            parts.append(blk[:, max(c0 - b0, 0):min(c1 - b0, GB)])
+        return torch.cat(parts, dim=1).to(dtype)
 
     def one():
         return solver.solve(None, m=m, n=n, dtype=dtype, generator=gen, gather=False)

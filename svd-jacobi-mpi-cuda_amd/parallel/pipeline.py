@@ -20,7 +20,9 @@ half 1 is issued after T11 and runs under the next round's T00' and T01'
 events of the tasks that last touched its two halves, so the two compute
 streams and the RCCL stream overlap as far as the data dependencies allow.
 Round 0 of every sweep also runs the within-super-block round robins
-(RR(slot 0) || RR(slot 1)).  Every block pair of the matrix still meets
+(RR(slot 0) || RR(slot 1)); the last round of a sweep (no exchange after it,
+the whole sweep on one GPU) runs the fully parallel order [T00 || T11],
+[T01 || T10].  Every block pair of the matrix still meets
 exactly once per sweep (checked by tests/test_pipeline_cpu.py).
 
 On CPU tensors (gloo tests) the same item list runs sequentially, with the
@@ -96,12 +98,14 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
                         [0] * h, stream, ((inc, ih), (stay, sh)))
 
         nxt = int(xslot[r + 1]) if r + 1 < R else None
-        plan.items += [task("T00", 0, 0, 0), task("T01", 0, 1, 0), task("T10", 1, 0, 1)]
-        if nxt is not None:
-            plan.items.append(Send(r + 1, nxt, 0))
-        plan.items.append(task("T11", 1, 1, 1))
-        if nxt is not None:
-            plan.items.append(Send(r + 1, nxt, 1))
+        if nxt is None:
+            # nothing to send after this round: the two fully parallel phases
+            # [T00 || T11], [T01 || T10]
+            plan.items += [task("T00", 0, 0, 0), task("T11", 1, 1, 1), task("T01", 0, 1, 0),
+                           task("T10", 1, 0, 1)]
+            continue
+        plan.items += [task("T00", 0, 0, 0), task("T01", 0, 1, 0), task("T10", 1, 0, 1),
+                       Send(r + 1, nxt, 0), task("T11", 1, 1, 1), Send(r + 1, nxt, 1)]
     return plan
 
 

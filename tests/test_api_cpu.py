@@ -85,8 +85,10 @@ def test_reference_ops_block_step_orthogonalises_pair():
 def test_qr_preconditioned_tall_skinny(method):
     """m >= 2n: A = QR, Jacobi on R, U = Q U_R (models/precondition.py)."""
     A = svdj.utils.inputs.random_dense(400, 96, seed=12)
-    res = svdj.svd(A, method=method, dtype=torch.float64)
+    res = svdj.svd(A, method=method, dtype=torch.float64, precondition="qr")
     assert res.info.get("precondition") == "qr"
+    assert svdj.svd(torch.rand(900, 100, dtype=torch.float64), method=method).info.get(
+        "precondition") == "qr"  # auto: m >= qr_ratio (8) n
     rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
     assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-10, rep
     assert res.U.shape == (400, 96)

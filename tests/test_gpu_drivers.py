@@ -77,7 +77,7 @@ def test_tall_skinny_bf16_qr_gpu(svdj, cuda):
     fp32 working copies, bf16 matrix cores (bf16x3) for the apply."""
     A = svdj.utils.inputs.random_dense(2048, 512, dtype=torch.float32, device=cuda,
                                        seed=14).to(torch.bfloat16)
-    res = svdj.svd(A, method="block")
+    res = svdj.svd(A, method="block", precondition="qr")
     assert res.converged and res.info["precondition"] == "qr" and res.info["mma"] == "bf16x3"
     assert res.U.dtype == torch.bfloat16 and res.U.shape == (2048, 512)
     rep = svdj.utils.metrics.verify(A.double(), res.U, res.S, res.V,
@@ -88,7 +88,7 @@ def test_tall_skinny_bf16_qr_gpu(svdj, cuda):
 
 def test_qr_preconditioned_fp32_gpu(svdj, cuda):
     A = svdj.utils.inputs.random_dense(3000, 640, dtype=torch.float32, device=cuda, seed=15)
-    res = svdj.svd(A, method="block")
+    res = svdj.svd(A, method="block", precondition="qr")
     plain = svdj.svd(A, method="block", precondition="none")
     ref = torch.linalg.svdvals(A.double().cpu())
     for r in (res, plain):
