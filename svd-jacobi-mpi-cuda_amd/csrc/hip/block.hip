@@ -190,7 +190,7 @@ __device__ __forceinline__ void rr_pair(int st, int a, int N, int& p, int& q) {
 //     while the fp64 (c, s) for Q are formed from t off the critical path
 //     (c^2 + s^2 = 1 to fp64 accuracy), barrier, DPP shift.
 #ifndef SVDJ_EVD_THREADS_32
-#define SVDJ_EVD_THREADS_32 512
+#define SVDJ_EVD_THREADS_32 1024  // measured: 64 us vs 78 us (512) per W=32 EVD
 #endif
 #ifndef SVDJ_EVD_THREADS_64
 #define SVDJ_EVD_THREADS_64 1024
@@ -253,6 +253,36 @@ __device__ __forceinline__ double rsqrt64(double x) {
   y = y * (1.5 - 0.5 * x * y * y);
   y = y * (1.5 - 0.5 * x * y * y);
   return y;
+}
+
+#ifdef SVDJ_EVD_PROFILE
+// Development instrumentation: per-phase cycle totals of one EVD workgroup
+// (pair 0), read back with svdj_debug_evd_profile().
+__device__ unsigned long long g_evd_prof[16];
+#define EVD_T(i) unsigned long long _t##i = (pair == 0 && (tid == 0 || tid == NT - 64)) ? clock64() : 0
+#define EVD_ACC(k, a, b) if (pair == 0 && (tid == 0 || tid == NT - 64)) atomicAdd(&g_evd_prof[(tid == 0 ? 0 : 8) + k], _t##b - _t##a)
+#else
+#define EVD_T(i)
+#define EVD_ACC(k, a, b)
+#endif
+
+// Circle-method players of slot a at step st (the same movement as the DPP
+// shifts of the register Q below: firsts move right, seconds left, player
+// N-1 fixed in slot 0).  Ring of N-1 positions; slot a >= 1 has its first at
+// position a-1 and its second at 2W-2-a; the player at position x after st
+// steps is ((x - st) mod (N-1) + 1) mod (N-1).  Checked against the DPP
+// movement by tests/test_schedule.py::test_evd_ring_matches_dpp_movement.
+template <int W>
+__device__ __forceinline__ int ring_player(int pos, int st) {
+  constexpr int R = 2 * W - 1;
+  int x = pos - st;
+  x += x < 0 ? R : 0;
+  return x + 1 == R ? 0 : x + 1;
+}
+template <int W>
+__device__ __forceinline__ void ring_slot(int a, int st, int& p, int& q) {
+  p = a == 0 ? 2 * W - 1 : ring_player<W>(a - 1, st);
+  q = ring_player<W>(2 * W - 2 - a, st);
 }
 
 template <typename T, int W>
@@ -332,18 +362,35 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     }
   }
 
-  // ---- fixed slot-pair blocks owned by this thread
-  int ba[MAXB], bb[MAXB];
+  // ---- fixed slot-pair blocks owned by this thread.  Off-diagonal blocks
+  // (a < b) are dealt round robin; the cheap diagonal blocks go to the
+  // threads left with one off-diagonal block fewer, so no thread carries an
+  // extra unit (W=64 on 1024 threads: 2016 off-diagonal + 64 diagonal blocks
+  // -> at most 2 units per thread instead of 3; the third unit of 32
+  // stragglers held up every barrier).
+  constexpr int NOFF = W * (W - 1) / 2;
+  constexpr int MAXOFF = (NOFF + NT - 1) / NT;
+  constexpr int F0 = NOFF - (MAXOFF - 1) * NT;  // first thread with a free unit
+  constexpr int NF = NT - F0;
+  constexpr int DPF = (W + NF - 1) / NF;         // diagonal blocks per free thread
+  static_assert(NF > 0 && DPF <= 2, "diagonal blocks must fit the free units");
+  int ba[MAXOFF], bb[MAXOFF], dg[DPF];
 #pragma unroll
-  for (int j = 0; j < MAXB; ++j) {
+  for (int j = 0; j < MAXOFF; ++j) {
     const int idx = tid + j * NT;
     ba[j] = bb[j] = -1;
-    if (idx < NBLK) {
+    if (idx < NOFF) {
+      // idx -> (a, b), a < b, row-major over the strict upper triangle
       int a = 0, base = 0;
-      while (idx >= base + (W - a)) { base += W - a; ++a; }
+      while (idx >= base + (W - 1 - a)) { base += W - 1 - a; ++a; }
       ba[j] = a;
-      bb[j] = a + (idx - base);
+      bb[j] = a + 1 + (idx - base);
     }
+  }
+#pragma unroll
+  for (int i = 0; i < DPF; ++i) {
+    const int d = (tid - F0) * DPF + i;
+    dg[i] = (tid >= F0 && d < W) ? d : -1;
   }
 
   // ---- slot layout state
@@ -363,62 +410,71 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   bool any = false;
   for (int sw = 0; sw < max_inner; ++sw) {
     for (int st = 0; st < N - 1; ++st) {
-      // (1) wave 0 solves the W rotations of this step and publishes them
+      EVD_T(0);
+      // (1) wave 0 solves the W rotations of this step and publishes them in
+      //     the data precision only (the fp64 form for Q is derived per lane
+      //     from t in (3), off this latency-critical single-wave phase)
       if (wave == 0 && lane < W) {
         const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[sidx(pf, ps)];
         T c = 1, s = 0, t = 0;
         RotRec<T> r;
-        r.c64 = 1.0;
+        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) sweep_rot = 1;
+        r.c64 = 0.0;
         r.s64 = 0.0;
-        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) {
-          if constexpr (sizeof(T) == 8) {
-            r.c64 = c;
-            r.s64 = s;
-          } else {
-            const double td = (double)t;
-            r.c64 = rsqrt64(1.0 + td * td);
-            r.s64 = td * r.c64;
-          }
-          sweep_rot = 1;
-        }
         r.c = c;
         r.s = s;
         r.t = t;
         r.pq = pf | (ps << 16);
         prm[slot] = r;
       }
+      EVD_T(1);
       __syncthreads();
-      // (2) G <- J^T G J on this thread's upper-triangle 2x2 blocks
+      EVD_T(2);
+      // (2) G <- J^T G J on this thread's blocks.  Players come from the ring
+      //     formula, so the G loads do not wait for the rotation records.
 #pragma unroll
-      for (int j = 0; j < MAXB; ++j) {
+      for (int j = 0; j < MAXOFF; ++j) {
         if (ba[j] < 0) continue;
-        const RotRec<T> A = prm[ba[j]];
-        const int p = A.pq & 0xffff, q = A.pq >> 16;
-        if (ba[j] == bb[j]) {
-          if (A.s != T(0)) {
-            const int ipq = sidx(p, q);
-            const T v = G[ipq];
-            G[p * LD + p] -= A.t * v;
-            G[q * LD + q] += A.t * v;
-            G[ipq] = T(0);
-          }
-        } else {
-          const RotRec<T> B = prm[bb[j]];
-          const int r = B.pq & 0xffff, u = B.pq >> 16;
-          const int i00 = sidx(p, r), i01 = sidx(p, u), i10 = sidx(q, r), i11 = sidx(q, u);
-          const T g00 = G[i00], g01 = G[i01], g10 = G[i10], g11 = G[i11];
-          const T h00 = A.c * g00 - A.s * g10, h01 = A.c * g01 - A.s * g11;
-          const T h10 = A.s * g00 + A.c * g10, h11 = A.s * g01 + A.c * g11;
-          G[i00] = B.c * h00 - B.s * h01;
-          G[i01] = B.s * h00 + B.c * h01;
-          G[i10] = B.c * h10 - B.s * h11;
-          G[i11] = B.s * h10 + B.c * h11;
+        int p, q, r, u;
+        ring_slot<W>(ba[j], st, p, q);
+        ring_slot<W>(bb[j], st, r, u);
+        const int i00 = sidx(p, r), i01 = sidx(p, u), i10 = sidx(q, r), i11 = sidx(q, u);
+        const T g00 = G[i00], g01 = G[i01], g10 = G[i10], g11 = G[i11];
+        const T ca = prm[ba[j]].c, sa = prm[ba[j]].s, cb = prm[bb[j]].c, sb = prm[bb[j]].s;
+        const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
+        const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
+        G[i00] = cb * h00 - sb * h01;
+        G[i01] = sb * h00 + cb * h01;
+        G[i10] = cb * h10 - sb * h11;
+        G[i11] = sb * h10 + cb * h11;
+      }
+#pragma unroll
+      for (int i = 0; i < DPF; ++i) {
+        if (dg[i] < 0) continue;
+        int p, q;
+        ring_slot<W>(dg[i], st, p, q);
+        const T ta = prm[dg[i]].t;
+        if (ta != T(0)) {
+          const int ipq = sidx(p, q);
+          const T v = G[ipq];
+          G[p * LD + p] -= ta * v;
+          G[q * LD + q] += ta * v;
+          G[ipq] = T(0);
         }
       }
-      // (3) Q <- Q J in registers (fp64)
+      // (3) Q <- Q J in registers (fp64): (c, s) from t, normalised in fp64
       {
-        const double c64 = prm[slot].c64, s64 = prm[slot].s64;
-        if (s64 != 0.0) {
+        const T tq = prm[slot].t;
+        if (tq != T(0)) {
+          double c64, s64;
+          if constexpr (sizeof(T) == 8) {
+            c64 = prm[slot].c;
+            s64 = prm[slot].s;
+          } else {
+            const double td = (double)tq;
+            c64 = rsqrt64(1.0 + td * td);
+            s64 = td * c64;
+          }
 #pragma unroll
           for (int i = 0; i < RPL; ++i) {
             const double x = qf[i], y = qs[i];
@@ -427,7 +483,9 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
           }
         }
       }
+      EVD_T(3);
       __syncthreads();
+      EVD_T(4);
       // (4) advance the round robin: firsts shift right, seconds shift left
 #pragma unroll
       for (int i = 0; i < RPL; ++i) {
@@ -444,6 +502,12 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         pf = nf;
         ps = ns;
       }
+      EVD_T(5);
+      EVD_ACC(0, 0, 1);
+      EVD_ACC(1, 1, 2);
+      EVD_ACC(2, 2, 3);
+      EVD_ACC(3, 3, 4);
+      EVD_ACC(4, 4, 5);
     }
     const int rot = sweep_rot;
     __syncthreads();
@@ -859,6 +923,17 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
 }  // namespace svdj
 
 using namespace svdj;
+
+#ifdef SVDJ_EVD_PROFILE
+extern "C" int svdj_debug_evd_profile(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_evd_prof), sizeof(g_evd_prof)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_evd_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
   return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);

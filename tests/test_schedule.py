@@ -115,3 +115,31 @@ def test_distributed_sweep_covers_every_block_pair_once(P, k):
                         seen.add(key)
         assert len(seen) == nblocks * (nblocks - 1) // 2
         assert plans[0].modes[0] == 1 and all(m == 0 for m in plans[0].modes[1:])
+
+
+def test_evd_ring_matches_dpp_movement():
+    """The EVD kernel computes slot players arithmetically (ring_slot in
+    csrc/hip/block.hip) for the G updates, while the register Q follows the
+    DPP shifts; both must describe the same circle-method movement and cover
+    every pair once per N-1 steps."""
+    def ring_player(W, pos, st):
+        R = 2 * W - 1
+        x = pos - st
+        x += R if x < 0 else 0
+        return 0 if x + 1 == R else x + 1
+
+    for W in (4, 8, 32, 64):
+        N = 2 * W
+        pf = [N - 1 if a == 0 else a for a in range(W)]
+        ps = [0 if a == 0 else N - 1 - a for a in range(W)]
+        seen = set()
+        for st in range(N - 1):
+            for a in range(W):
+                p = N - 1 if a == 0 else ring_player(W, a - 1, st)
+                q = ring_player(W, 2 * W - 2 - a, st)
+                assert (p, q) == (pf[a], ps[a])
+                seen.add((min(p, q), max(p, q)))
+            nf = [pf[a] if a == 0 else (ps[0] if a == 1 else pf[a - 1]) for a in range(W)]
+            ns = [pf[a] if a == W - 1 else ps[a + 1] for a in range(W)]
+            pf, ps = nf, ns
+        assert len(seen) == N * (N - 1) // 2
