@@ -543,8 +543,18 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 namespace svdj {
 
 // ------------------------------------------------------------------ apply
+#ifndef SVDJ_APPLY_QPD
+#define SVDJ_APPLY_QPD 8
+#endif
+#ifndef SVDJ_APPLY_THREADS_64
+#define SVDJ_APPLY_THREADS_64 256
+#endif
 template <typename T, int W>
-__global__ __launch_bounds__(kApplyThreads) void apply_kernel(
+__host__ __device__ constexpr int apply_threads() {
+  return (W == 64 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_64 : kApplyThreads;
+}
+template <typename T, int W>
+__global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     T* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, T* __restrict__ V,
     int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs, const T* __restrict__ Qall,
     const int32_t* __restrict__ skip) {
@@ -555,7 +565,8 @@ __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
   constexpr int NK = N / KG;   // k values per lane
   constexpr int NCT = N / TL;  // output column tiles
   constexpr int LDQ = N + (sizeof(T) == 8 ? 16 : 0);
-  constexpr int WAVES = kApplyThreads / SVDJ_WAVE;
+  constexpr int NTH = apply_threads<T, W>();
+  constexpr int WAVES = NTH / SVDJ_WAVE;
   __shared__ T Qs[N * LDQ];
 
   const int pair = blockIdx.x;
@@ -577,7 +588,7 @@ __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
     r_end = min(n_v, r_begin + rows_v);
   }
   const T* Qg = Qall + (size_t)pair * N * N;
-  for (int i = threadIdx.x; i < N * N; i += kApplyThreads) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
+  for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -616,10 +627,20 @@ __global__ __launch_bounds__(kApplyThreads) void apply_kernel(
 #pragma unroll kCtUnroll
     for (int ct = 0; ct < NCT; ++ct) {
       typename M::acc_t acc = M::zero();
+      // Q fragments are read SVDJ_APPLY_QPD k-steps ahead of their MFMA
+      // (sched_barrier keeps the order; just in time, each ds_read's latency
+      // sat between two dependent MFMAs).  Two interleaved accumulation
+      // chains per wave were measured slower (1269 vs 1145 us, W=64).
+      constexpr int PD = SVDJ_APPLY_QPD < NK ? SVDJ_APPLY_QPD : NK;
+      T qa[PD];
+#pragma unroll
+      for (int i = 0; i < PD; ++i) qa[i] = Qs[(i * KG + kg) * LDQ + ct * TL + lc];
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
-        const T a = Qs[(kk * KG + kg) * LDQ + ct * TL + lc];
+        const T a = qa[kk % PD];
+        if (kk + PD < NK) qa[kk % PD] = Qs[((kk + PD) * KG + kg) * LDQ + ct * TL + lc];
         acc = M::mfma(a, xv[kk], acc);
+        __builtin_amdgcn_sched_barrier(0);
       }
       const int c0 = ct * TL;
       T* dst = (c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld);
@@ -913,7 +934,7 @@ static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
         continue;
       }
     }
-    hipLaunchKernelGGL((apply_kernel<T, W>), apply_grid, dim3(kApplyThreads), 0, st, A, lda,
+    hipLaunchKernelGGL((apply_kernel<T, W>), apply_grid, dim3(apply_threads<T, W>()), 0, st, A, lda,
                        g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0, pr, Q, skip);
     SVDJ_LAUNCH_CHECK();
   }
@@ -1058,7 +1079,7 @@ extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld
     hipLaunchKernelGGL((apply_split_kernel<32, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
   else if (dtype == 0 && mma == 0 && W == 64)
-    hipLaunchKernelGGL((apply_kernel<float, 64>), grid, blk, 0, st, (float*)X, ld, chunks,
+    hipLaunchKernelGGL((apply_kernel<float, 64>), grid, dim3(apply_threads<float, 64>()), 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
   else if (dtype == 0 && mma == 0 && W == 32)
     hipLaunchKernelGGL((apply_kernel<float, 32>), grid, blk, 0, st, (float*)X, ld, chunks,

@@ -25,9 +25,41 @@ def use_qr(cfg: SolverConfig, m: int, n: int) -> bool:
     return m >= cfg.qr_ratio * n and n >= 64
 
 
-def qr(A: torch.Tensor, dtype: torch.dtype):
-    """Reduced QR in the working precision on A's device."""
-    Q, R = torch.linalg.qr(A.to(dtype), mode="reduced")
+def qr(A: torch.Tensor, dtype: torch.dtype, method: str = "auto"):
+    """Reduced QR in the working precision on A's device.
+
+    ``cholqr2``: CholeskyQR2 -- twice (G = Q^T Q, G = L L^T, Q <- Q L^-T),
+    R = L2^T L1^T.  Everything is GEMM / TRSM shaped (hipBLASLt, rocBLAS)
+    and stable while kappa(A)^2 eps < 1.  ``householder``: torch.linalg.qr
+    (rocSOLVER geqrf on the GPU, which made QR cost more than it saved at
+    32768 x 8192).  ``auto``: CholeskyQR2 on the GPU, Householder if the Gram
+    is not numerically positive definite (or on the CPU)."""
+    A = A.to(dtype)
+    if method in ("auto", "cholqr2") and (A.is_cuda or method == "cholqr2"):
+        out = _cholqr2(A)
+        if out is not None:
+            return out
+        if method == "cholqr2":
+            raise RuntimeError("CholeskyQR2 failed: Gram not positive definite (ill-conditioned A)")
+    Q, R = torch.linalg.qr(A, mode="reduced")
+    return Q, R
+
+
+def _cholqr2(A: torch.Tensor):
+    """None when A is too ill-conditioned for CholeskyQR2 (kappa >~ eps^-1/2,
+    estimated from the first Cholesky factor's pivots)."""
+    eps = torch.finfo(A.dtype).eps
+    Q, R = A, None
+    for it in range(2):
+        L, info = torch.linalg.cholesky_ex(Q.t() @ Q)
+        if int(info) != 0 or not bool(torch.isfinite(L).all()):
+            return None
+        if it == 0:
+            d = torch.diagonal(L).abs()
+            if float(d.min()) <= eps ** 0.5 * float(d.max()):
+                return None
+        Q = torch.linalg.solve_triangular(L.t(), Q, upper=True, left=False)  # Q L^-T
+        R = L.t() if R is None else L.t() @ R
     return Q, R
 
 

@@ -112,3 +112,18 @@ def test_bf16_mode_cpu():
     assert rep["residual_rel"] < 2e-2, rep  # U, V rounded to bf16
     cfg = svdj.SolverConfig(dtype=torch.bfloat16)
     assert cfg.resolved_dtype(None) == torch.float32 and cfg.precision_dtype(None) == torch.bfloat16
+
+
+def test_cholqr2_matches_householder():
+    pre = svdj.models.precondition
+    A = svdj.utils.inputs.random_dense(500, 80, seed=16)
+    Q, R = pre.qr(A, torch.float64, method="cholqr2")
+    torch.testing.assert_close(Q @ R, A, rtol=1e-12, atol=1e-12)
+    eye = torch.eye(80, dtype=torch.float64)
+    assert (Q.t() @ Q - eye).abs().max() < 1e-13
+    assert torch.allclose(R, torch.triu(R))
+    B = A @ torch.diag(torch.logspace(0, -12, 80, dtype=torch.float64))  # kappa ~ 1e12
+    with pytest.raises(RuntimeError):
+        pre.qr(B, torch.float64, method="cholqr2")
+    Q2, R2 = pre.qr(B, torch.float64, method="householder")
+    torch.testing.assert_close(Q2 @ R2, B, rtol=1e-12, atol=1e-12)

@@ -16,4 +16,4 @@ for x in list(csv.DictReader(open(sys.argv[1])))[:4]:
     print("  %-48s %6s %8.1f us" % (x['Name'][:48], x['Calls'], float(x['AverageNs'])/1e3))
 PY
 }
-run w64_x6 64 bf16x6 && run w32_x6 32 bf16x6
+run w64_nat 64 native && run w32_nat 32 native
