@@ -55,10 +55,9 @@ class SolverConfig:
     sort: bool = False              # reference returns unsorted sigma
     mma: str = "auto"               # block apply matrix cores: auto | native | bf16x6 | bf16x3
     precondition: str = "auto"      # auto | qr | none  (QR first when m >= qr_ratio * n)
-    # Measured on MI355X, 32768 x 8192 fp32: Jacobi on A directly 2.6 s, QR (torch ->
-    # rocSOLVER geqrf) + Jacobi on R 5.4 s -- the library QR is the bottleneck at m = 4n,
-    # so "auto" only factors very tall inputs.
-    qr_ratio: float = 8.0
+    # Measured on MI355X, 32768 x 8192 fp32: Jacobi on A directly 2.27-2.6 s; CholeskyQR2
+    # + Jacobi on R + U = Q U_R 1.99 s (Householder QR via rocSOLVER geqrf: 5.4 s).
+    qr_ratio: float = 2.0
     chains: int = 2                 # block path: independent step chains on separate streams
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     checkpoint_dir: str | None = None

@@ -88,7 +88,7 @@ def test_qr_preconditioned_tall_skinny(method):
     res = svdj.svd(A, method=method, dtype=torch.float64, precondition="qr")
     assert res.info.get("precondition") == "qr"
     assert svdj.svd(torch.rand(900, 100, dtype=torch.float64), method=method).info.get(
-        "precondition") == "qr"  # auto: m >= qr_ratio (8) n
+        "precondition") == "qr"  # auto: m >= qr_ratio (2) n
     rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
     assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-10, rep
     assert res.U.shape == (400, 96)
