@@ -362,19 +362,15 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     }
   }
 
-  // ---- fixed slot-pair blocks owned by this thread.  Off-diagonal blocks
-  // (a < b) are dealt round robin; the cheap diagonal blocks go to the
-  // threads left with one off-diagonal block fewer, so no thread carries an
-  // extra unit (W=64 on 1024 threads: 2016 off-diagonal + 64 diagonal blocks
-  // -> at most 2 units per thread instead of 3; the third unit of 32
-  // stragglers held up every barrier).
+  // ---- off-diagonal slot-pair blocks (a < b) owned by this thread, dealt
+  // round robin (W=64: 2016 blocks -> 2 per thread).  The diagonal blocks
+  // are updated by wave 0 in phase (1): they hold exactly the three entries
+  // the rotation solve reads, and no off-diagonal block touches them.  (As a
+  // separate unit on the last wave's spare lanes they diverged from the
+  // off-diagonal path: ~3700 cycles/step in that wave vs ~1700 elsewhere.)
   constexpr int NOFF = W * (W - 1) / 2;
   constexpr int MAXOFF = (NOFF + NT - 1) / NT;
-  constexpr int F0 = NOFF - (MAXOFF - 1) * NT;  // first thread with a free unit
-  constexpr int NF = NT - F0;
-  constexpr int DPF = (W + NF - 1) / NF;         // diagonal blocks per free thread
-  static_assert(NF > 0 && DPF <= 2, "diagonal blocks must fit the free units");
-  int ba[MAXOFF], bb[MAXOFF], dg[DPF];
+  int ba[MAXOFF], bb[MAXOFF];
 #pragma unroll
   for (int j = 0; j < MAXOFF; ++j) {
     const int idx = tid + j * NT;
@@ -386,11 +382,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       ba[j] = a;
       bb[j] = a + 1 + (idx - base);
     }
-  }
-#pragma unroll
-  for (int i = 0; i < DPF; ++i) {
-    const int d = (tid - F0) * DPF + i;
-    dg[i] = (tid >= F0 && d < W) ? d : -1;
   }
 
   // ---- slot layout state
@@ -415,10 +406,17 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       //     the data precision only (the fp64 form for Q is derived per lane
       //     from t in (3), off this latency-critical single-wave phase)
       if (wave == 0 && lane < W) {
-        const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[sidx(pf, ps)];
+        const int ipq = sidx(pf, ps);
+        const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[ipq];
         T c = 1, s = 0, t = 0;
         RotRec<T> r;
-        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) sweep_rot = 1;
+        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) {
+          sweep_rot = 1;
+          // this slot's diagonal block (exact update)
+          G[pf * LD + pf] = gpp - t * gpq;
+          G[ps * LD + ps] = gqq + t * gpq;
+          G[ipq] = T(0);
+        }
         r.c64 = 0.0;
         r.s64 = 0.0;
         r.c = c;
@@ -447,20 +445,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         G[i01] = sb * h00 + cb * h01;
         G[i10] = cb * h10 - sb * h11;
         G[i11] = sb * h10 + cb * h11;
-      }
-#pragma unroll
-      for (int i = 0; i < DPF; ++i) {
-        if (dg[i] < 0) continue;
-        int p, q;
-        ring_slot<W>(dg[i], st, p, q);
-        const T ta = prm[dg[i]].t;
-        if (ta != T(0)) {
-          const int ipq = sidx(p, q);
-          const T v = G[ipq];
-          G[p * LD + p] -= ta * v;
-          G[q * LD + q] += ta * v;
-          G[ipq] = T(0);
-        }
       }
       // (3) Q <- Q J in registers (fp64): (c, s) from t, normalised in fp64
       {

@@ -13,5 +13,4 @@ for x in csv.DictReader(open(sys.argv[1])):
 PY
 }
 L=$R/svd-jacobi-mpi-cuda_amd/lib
-run succ32 $L/libsvdj_hip.so 32 && run succ64 $L/libsvdj_hip.so 64 && \
-run twobar32 $L/variants/libsvdj_hip_twobar.so 32 && run twobar64 $L/variants/libsvdj_hip_twobar.so 64
+run w32 $L/libsvdj_hip.so 32 && run w64 $L/libsvdj_hip.so 64
