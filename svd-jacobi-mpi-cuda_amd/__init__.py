@@ -15,7 +15,7 @@ from __future__ import annotations
 __version__ = "0.1.0"
 
 from . import cli, config, ops, models, parallel, utils  # noqa: F401
-from .api import gesvd, svd  # noqa: F401
+from .api import gesvd, svd, svd_on_the_fly  # noqa: F401
 from .config import SolverConfig, SVDOptions  # noqa: F401
 from .models.base import SVDResult  # noqa: F401
 

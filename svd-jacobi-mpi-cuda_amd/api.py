@@ -100,3 +100,20 @@ def gesvd(jobu, jobv, m: int, n: int, A: torch.Tensor, lda: int, s: torch.Tensor
         Vcm = flatV[: ldv * n].view(n, ldv)[:, :n].t()
         Vcm.copy_(res.V[:n, :n].to(V.dtype))
     return res
+
+
+def svd_on_the_fly(m: int, n: int, generator, comm=None, jobu=SVDOptions.AllVec,
+                   jobv=SVDOptions.AllVec, dtype: torch.dtype = torch.float32,
+                   config: SolverConfig | None = None, gather: bool = True) -> SVDResult:
+    """Distributed SVD of a matrix that is never assembled on one rank:
+    ``generator(c0, c1)`` returns columns c0..c1-1 (m x (c1-c0)) of a fixed
+    matrix on the calling rank's device, and every rank generates only the
+    super-blocks it owns.  The reference declares this entry point
+    (``omp_mpi_dgesvd_on_the_fly_matrices``, lib/JacobiMethods.cuh:64-72) but
+    never defines it.  ``comm`` defaults to a fresh Communicator (one process
+    per GPU, RCCL; gloo on CPU)."""
+    from .parallel import Communicator, DistributedBlockJacobi
+
+    solver = DistributedBlockJacobi(config or SolverConfig(), comm or Communicator())
+    return solver.solve(None, jobu, jobv, m=m, n=n, dtype=dtype, generator=generator,
+                        gather=gather)

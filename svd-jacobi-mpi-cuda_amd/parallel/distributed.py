@@ -322,6 +322,24 @@ class DistributedBlockJacobi(Solver):
         else:
             comm.sendrecv([], [(At, 0)])
 
+    def roundtrip(self, A: torch.Tensor | None, m: int, n: int, dtype=torch.float64):
+        """Scatter root-owned A over the ranks' resident super-blocks and gather
+        it back unchanged (rank 0 returns the (m, n) matrix, others None).
+
+        The reference names this check ``test_local_matrix_distribution_*``
+        and has the round-trip comparisons commented out
+        (reference main.cu:630-643, 866-877, 1605-1609); here it is a method
+        the tests call."""
+        comm = self.comm
+        geo = self.geometry(m, n, dtype)
+        B, m_pad = geo["B"], geo["m_pad"]
+        held = [int(tournament(comm.world).held[0, comm.rank, s]) for s in range(2)]
+        At = torch.zeros(2 * B, m_pad, dtype=dtype, device=comm.device)
+        self._distribute(A, None, At, held, m, n, B, dtype)
+        sigma = torch.zeros(2 * B, dtype=dtype, device=comm.device)
+        U, _, _ = self._gather(At, None, sigma, held, m, n, B, dtype, False, True)
+        return U
+
     def _gather(self, At, Vt, sigma, held, m, n, B, dtype, want_v, want_u):
         comm = self.comm
         ids = torch.tensor(held, dtype=torch.int64, device=At.device)

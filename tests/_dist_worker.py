@@ -18,6 +18,38 @@ def main():
                             precondition="qr" if mode.endswith("qr") else "none")
     solver = DistributedBlockJacobi(cfg, comm)
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=9)
+    if mode == "roundtrip":  # reference test_local_matrix_distribution_* parity
+        U = solver.roundtrip(A if comm.rank == 0 else None, m, n)
+        if comm.rank == 0:
+            with open(out, "w") as f:
+                json.dump({"max_err": float((U - A).abs().max()), "world": comm.world}, f)
+        comm.destroy()
+        return
+    if mode == "isend":  # reference test_MPI_Isend_Recv parity: ring exchange
+        x = torch.full((5,), float(comm.rank), dtype=torch.float64)
+        y = torch.empty(5, dtype=torch.float64)
+        nxt, prv = (comm.rank + 1) % comm.world, (comm.rank - 1) % comm.world
+        for w in comm.isendrecv([(x, nxt)], [(y, prv)]):
+            w.wait()
+        ok = bool((y == prv).all())
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64)
+        import torch.distributed as dist
+        dist.all_reduce(t)
+        if comm.rank == 0:
+            with open(out, "w") as f:
+                json.dump({"ok_ranks": float(t[0]), "world": comm.world}, f)
+        comm.destroy()
+        return
+    if mode == "otf":  # on-the-fly generated input through the public API
+        res = svdj.svd_on_the_fly(m, n, lambda c0, c1: A[:, c0:c1], comm=comm,
+                                  dtype=torch.float64, config=cfg)
+        if comm.rank == 0:
+            rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+            rep.update(sweeps=res.sweeps, converged=res.converged, world=comm.world)
+            with open(out, "w") as f:
+                json.dump(rep, f)
+        comm.destroy()
+        return
     if mode in ("root", "rootqr"):
         res = solver.solve(A if comm.rank == 0 else None)
     else:

@@ -48,3 +48,21 @@ def test_distributed_qr_preconditioned(mode, tmp_path):
     rep = _run(2, 300, 128, 32, tmp_path, mode=mode)
     assert rep["converged"] and rep["residual_rel"] < 1e-12, rep
     assert rep["orth_u_fro"] < 1e-10 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_matrix_distribution_roundtrip(world, tmp_path):
+    """Scatter root-owned A to the resident super-blocks and gather it back."""
+    rep = _run(world, 130, 100, 32, tmp_path, mode="roundtrip")
+    assert rep["max_err"] == 0.0 and rep["world"] == world
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_isend_irecv_ring(world, tmp_path):
+    rep = _run(world, 8, 8, 32, tmp_path, mode="isend")
+    assert rep["ok_ranks"] == world
+
+
+def test_svd_on_the_fly_api(tmp_path):
+    rep = _run(2, 170, 128, 32, tmp_path, mode="otf")
+    assert rep["converged"] and rep["residual_rel"] < 1e-12, rep
