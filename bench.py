@@ -81,6 +81,8 @@ def main():
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
     p.add_argument("--chains", type=int, default=2)
+    p.add_argument("--no-stagger", action="store_true",
+                   help="issue the two step chains independently (lockstep) instead of offset")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
                    help="block apply matrix cores (auto = native f32/f64 MFMA; bf16x6/bf16x3 "
                         "split modes are faster but not fp32-accurate on every input)")
@@ -105,6 +107,7 @@ def main():
     m = a.m or n
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
+                            stagger=not a.no_stagger,
                             precondition=a.precondition)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device

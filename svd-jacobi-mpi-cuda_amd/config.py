@@ -59,6 +59,7 @@ class SolverConfig:
     # + Jacobi on R + U = Q U_R 1.99 s (Householder QR via rocSOLVER geqrf: 5.4 s).
     qr_ratio: float = 2.0
     chains: int = 2                 # block path: independent step chains on separate streams
+    stagger: bool = True            # offset the two chains by an EVD (svdj_block_steps2)
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)

@@ -841,11 +841,104 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   return ((slabs + 255) / 256 * 256) + 2 * ((q + 255) / 256 * 256) + 2 * ((sk + 255) / 256 * 256);
 }
 
-// Step pipeline on the caller's stream: gram(s) -> evd(s) -> apply(s).
-// Concurrency comes from the caller running independent chains on separate
-// streams (parallel/distributed.py); each chain owns its own workspace.
-// Q and the skip flags are double-buffered so evd(s+1) never overwrites what
-// apply(s) may still read if a caller splits the step across streams.
+// One chain of steps: resident buffers, its pair list and its workspace.
+template <typename T>
+struct Chain {
+  int m_pad, lda, n_v, ldv, P, steps;
+  T *A, *V, *D;
+  const int32_t* pairs;
+  const int32_t* modes;
+  Geometry g;
+  T* slabs;
+  T* Qb[2];
+  int32_t* skipb[2];
+  hipStream_t st;
+};
+
+template <typename T, int W>
+static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
+                      const int32_t* pairs, int P, int steps, const int32_t* modes, void* ws,
+                      size_t ws_bytes, int mma, hipStream_t st) {
+  const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad);
+  if (ws_bytes < need) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, need);
+    return -4;
+  }
+  if (mma != 0 && sizeof(T) != 4) {
+    set_error("split-bf16 matrix-core modes need fp32 data");
+    return -3;
+  }
+  c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
+  c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
+  c.g = make_geometry(P, m_pad, V ? n_v : 0);
+  char* w = (char*)ws;
+  c.slabs = (T*)w;
+  w += ((size_t)P * c.g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
+  const size_t qstride = ((size_t)P * 4 * W * W * sizeof(T) + 255) / 256 * 256;
+  c.Qb[0] = (T*)w;
+  c.Qb[1] = (T*)(w + qstride);
+  w += 2 * qstride;
+  const size_t kstride = ((size_t)P * sizeof(int32_t) + 255) / 256 * 256;
+  c.skipb[0] = (int32_t*)w;
+  c.skipb[1] = (int32_t*)(w + kstride);
+  return 0;
+}
+
+// Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
+// never overwrites what apply(s) may still read).
+template <typename T, int W>
+static int launch_gram_evd(const Chain<T>& c, int s, double tol, int max_inner, uint32_t* metric) {
+  const int b = s & 1;
+  const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
+  const int full = c.modes ? c.modes[s] : 0;
+  if (full)
+    hipLaunchKernelGGL((gram_kernel<T, W, true>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
+                       c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  else
+    hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
+                       c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  SVDJ_LAUNCH_CHECK();
+#if defined(SVDJ_EVD2)
+  // Two-level EVD (evd2.hpp): measured slower on MI355X, kept opt-in.
+  if constexpr (W == 32)
+    hipLaunchKernelGGL((evd2_kernel<T>), dim3(c.P), dim3(kEvd2Threads), 0, c.st, pr, full,
+                       c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, max_inner, metric);
+  else
+#endif
+    hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
+                       c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, max_inner, metric);
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T, int W>
+static int launch_apply(const Chain<T>& c, int s, int mma) {
+  const int b = s & 1;
+  const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
+  const dim3 grid(c.P, c.g.a_chunks + c.g.v_chunks);
+  const int nv = c.V ? c.n_v : 0;
+  if constexpr (sizeof(T) == 4) {
+    if (mma == 1 || mma == 2) {
+      if (mma == 1)
+        hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
+                           pr, c.Qb[b], c.skipb[b]);
+      else
+        hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
+                           pr, c.Qb[b], c.skipb[b]);
+      SVDJ_LAUNCH_CHECK();
+      return 0;
+    }
+  }
+  hipLaunchKernelGGL((apply_kernel<T, W>), grid, dim3(apply_threads<T, W>()), 0, c.st, c.A, c.lda,
+                     c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv, pr, c.Qb[b],
+                     c.skipb[b]);
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
+// Step pipeline on the chain's stream: gram(s) -> evd(s) -> apply(s).
 //
 // mma: 0 = native matrix cores for the data type (f32 / f64 MFMA),
 //      1 = fp32 data on bf16 MFMA, 3-way split (fp32-level accuracy),
@@ -856,71 +949,66 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
 // (a dominant column, or Q ~ I late in the iteration): on U(0,1) 8192^2 the
 // final ||AV - US||/||A|| is 6.5e-4 vs 8e-6 native.  Native is the default.
 template <typename T, int W>
-static int block_steps_t(int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
-                         const int32_t* pairs, int P, int steps, const int32_t* modes,
-                         double tol, int max_inner, void* ws, size_t ws_bytes,
-                         uint32_t* metric, int mma, hipStream_t st) {
-  const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad);
-  if (ws_bytes < need) {
-    set_error("workspace too small: %zu < %zu", ws_bytes, need);
-    return -4;
+static int block_steps_t(const Chain<T>& c, double tol, int max_inner, uint32_t* metric, int mma) {
+  for (int s = 0; s < c.steps; ++s) {
+    int rc = launch_gram_evd<T, W>(c, s, tol, max_inner, metric);
+    if (!rc) rc = launch_apply<T, W>(c, s, mma);
+    if (rc) return rc;
   }
-  if (mma != 0 && sizeof(T) != 4) {
-    set_error("split-bf16 matrix-core modes need fp32 data");
-    return -3;
+  return 0;
+}
+
+// Recycled cross-stream events of the staggered two-chain issue (one ring per
+// device; a wait captures the event's state when it is enqueued, so an event
+// can be re-recorded once its waits are issued).
+static hipEvent_t* stagger_events(int& n) {
+  constexpr int kMaxDev = 64, kRing = 64;
+  static hipEvent_t ev[kMaxDev][kRing];
+  static bool made[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!made[dev]) {
+    for (int i = 0; i < kRing; ++i)
+      if (hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess) return nullptr;
+    made[dev] = true;
   }
-  Geometry g = make_geometry(P, m_pad, V ? n_v : 0);
-  char* w = (char*)ws;
-  T* slabs = (T*)w;
-  w += ((size_t)P * g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
-  const size_t qstride = ((size_t)P * 4 * W * W * sizeof(T) + 255) / 256 * 256;
-  T* Qb[2] = {(T*)w, (T*)(w + qstride)};
-  w += 2 * qstride;
-  const size_t kstride = ((size_t)P * sizeof(int32_t) + 255) / 256 * 256;
-  int32_t* skipb[2] = {(int32_t*)w, (int32_t*)(w + kstride)};
-  const dim3 apply_grid(P, g.a_chunks + g.v_chunks);
-  for (int s = 0; s < steps; ++s) {
-    const int b = s & 1;
-    T* Q = Qb[b];
-    int32_t* skip = skipb[b];
-    const int32_t* pr = pairs + (size_t)s * P * 2;
-    const int full = modes ? modes[s] : 0;
-    if (full)
-      hipLaunchKernelGGL((gram_kernel<T, W, true>), dim3(P, g.gchunks), dim3(kGramThreads), 0, st,
-                         A, lda, m_pad, pr, g.grows, slabs);
-    else
-      hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(P, g.gchunks), dim3(kGramThreads), 0,
-                         st, A, lda, m_pad, pr, g.grows, slabs);
-    SVDJ_LAUNCH_CHECK();
-#if defined(SVDJ_EVD2)
-    // Two-level EVD (evd2.hpp): measured slower on MI355X, kept opt-in.
-    if constexpr (W == 32)
-      hipLaunchKernelGGL((evd2_kernel<T>), dim3(P), dim3(kEvd2Threads), 0, st, pr, full, slabs,
-                         g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
-    else
-#endif
-      hipLaunchKernelGGL((evd_kernel<T, W>), dim3(P), dim3(evd_threads(W)), 0, st, pr, full,
-                         slabs, g.gchunks, D, Q, skip, (T)tol, max_inner, metric);
-    SVDJ_LAUNCH_CHECK();
-    if constexpr (sizeof(T) == 4) {
-      if (mma == 1) {
-        hipLaunchKernelGGL((apply_split_kernel<W, 3>), apply_grid, dim3(kApplyThreads), 0, st,
-                           A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0,
-                           pr, Q, skip);
-        SVDJ_LAUNCH_CHECK();
-        continue;
-      }
-      if (mma == 2) {
-        hipLaunchKernelGGL((apply_split_kernel<W, 2>), apply_grid, dim3(kApplyThreads), 0, st,
-                           A, lda, g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0,
-                           pr, Q, skip);
-        SVDJ_LAUNCH_CHECK();
-        continue;
-      }
+  n = kRing;
+  return ev[dev];
+}
+
+// Two independent chains on two streams, staggered: chain B's step s starts
+// when chain A's EVD of step s has finished.  Issued separately the chains
+// run in lockstep (identical steps): both EVDs -- one workgroup per pair,
+// most CUs idle -- overlap each other, and so do both applies.  Staggered,
+// B's gram/EVD run under A's apply and A's next gram/EVD under B's apply,
+// which matters when the per-GPU work is small (many GPUs): the EVD latency
+// is then the critical path (tools/gpu_latency_sim.sh, tools/trace_gaps.py).
+template <typename T, int W>
+static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int max_inner,
+                          uint32_t* metric, int mma) {
+  int ne = 0;
+  hipEvent_t* ev = stagger_events(ne);
+  if (!ev) {
+    set_error("stagger events unavailable");
+    return -100;
+  }
+  const int n = a.steps > b.steps ? a.steps : b.steps;
+  for (int s = 0; s < n; ++s) {
+    int rc = 0;
+    if (s < a.steps) {
+      rc = launch_gram_evd<T, W>(a, s, tol, max_inner, metric);
+      if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
+      if (!rc) rc = launch_apply<T, W>(a, s, mma);
     }
-    hipLaunchKernelGGL((apply_kernel<T, W>), apply_grid, dim3(apply_threads<T, W>()), 0, st, A, lda,
-                       g.a_chunks, g.rows_a, m_pad, V, ldv, g.rows_v, V ? n_v : 0, pr, Q, skip);
-    SVDJ_LAUNCH_CHECK();
+    if (!rc && s < b.steps) {
+      if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
+      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, max_inner, metric);
+      if (!rc) rc = launch_apply<T, W>(b, s, mma);
+    }
+    if (rc) {
+      if (rc == -100) set_error("stagger event record/wait failed");
+      return rc;
+    }
   }
   return 0;
 }
@@ -944,10 +1032,7 @@ extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad)
   return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);
 }
 
-extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
-                                int ldv, void* D, const int32_t* pairs, int P, int steps,
-                                const int32_t* modes, double tol, int max_inner, void* ws,
-                                size_t ws_bytes, uint32_t* metric, int mma, void* stream) {
+static int check_dims(int m_pad, int lda, const void* V, int n_v, int ldv, int mma) {
   if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad) {
     set_error("bad m_pad/lda %d/%d", m_pad, lda);
     return -2;
@@ -960,20 +1045,67 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
     set_error("bad matrix-core mode %d", mma);
     return -2;
   }
+  return 0;
+}
+
+template <typename T, int W>
+static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D,
+                          const int32_t* pairs, int P, int steps, const int32_t* modes,
+                          double tol, int max_inner, void* ws, size_t ws_bytes, uint32_t* metric,
+                          int mma, void* stream, const int32_t* pairs2, int P2, int steps2,
+                          const int32_t* modes2, void* ws2, size_t ws2_bytes, void* stream2) {
+  Chain<T> a, b;
+  int rc = chain_init<T, W>(a, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
+                            ws, ws_bytes, mma, (hipStream_t)stream);
+  if (rc) return rc;
+  if (!pairs2 || P2 <= 0 || steps2 <= 0) return block_steps_t<T, W>(a, tol, max_inner, metric, mma);
+  if (ws2 == ws || stream2 == stream) {
+    set_error("staggered chains need distinct workspaces and streams");
+    return -2;
+  }
+  rc = chain_init<T, W>(b, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs2, P2, steps2, modes2,
+                        ws2, ws2_bytes, mma, (hipStream_t)stream2);
+  if (rc) return rc;
+  return block_steps2_t<T, W>(a, b, tol, max_inner, metric, mma);
+}
+
+static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v, int ldv,
+                     void* D, const int32_t* pairs, int P, int steps, const int32_t* modes,
+                     double tol, int max_inner, void* ws, size_t ws_bytes, uint32_t* metric,
+                     int mma, void* stream, const int32_t* pairs2, int P2, int steps2,
+                     const int32_t* modes2, void* ws2, size_t ws2_bytes, void* stream2) {
+  int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
+  if (rc) return rc;
   if (P <= 0 || steps < 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == 0 && W == 32)
-    return block_steps_t<float, 32>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
-                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, mma, st);
-  if (dtype == 0 && W == 64)
-    return block_steps_t<float, 64>(m_pad, (float*)A, lda, (float*)V, n_v, ldv, (float*)D, pairs,
-                                    P, steps, modes, tol, max_inner, ws, ws_bytes, metric, mma, st);
-  if (dtype == 1 && W == 32)
-    return block_steps_t<double, 32>(m_pad, (double*)A, lda, (double*)V, n_v, ldv, (double*)D,
-                                     pairs, P, steps, modes, tol, max_inner, ws, ws_bytes,
-                                     metric, mma, st);
+#define SVDJ_STEPS_ARGS                                                                       \
+  m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol, max_inner, ws, ws_bytes, metric, \
+      mma, stream, pairs2, P2, steps2, modes2, ws2, ws2_bytes, stream2
+  if (dtype == 0 && W == 32) return steps_dispatch<float, 32>(SVDJ_STEPS_ARGS);
+  if (dtype == 0 && W == 64) return steps_dispatch<float, 64>(SVDJ_STEPS_ARGS);
+  if (dtype == 1 && W == 32) return steps_dispatch<double, 32>(SVDJ_STEPS_ARGS);
+#undef SVDJ_STEPS_ARGS
   set_error("unsupported (dtype=%d, W=%d); supported: fp32 W in {32,64}, fp64 W=32", dtype, W);
   return -3;
+}
+
+extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                int ldv, void* D, const int32_t* pairs, int P, int steps,
+                                const int32_t* modes, double tol, int max_inner, void* ws,
+                                size_t ws_bytes, uint32_t* metric, int mma, void* stream) {
+  return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
+                   max_inner, ws, ws_bytes, metric, mma, stream, nullptr, 0, 0, nullptr, nullptr,
+                   0, nullptr);
+}
+
+extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                 int ldv, void* D, const int32_t* pairs, int P, int steps,
+                                 const int32_t* modes, void* ws, size_t ws_bytes, void* stream,
+                                 const int32_t* pairs2, int P2, int steps2, const int32_t* modes2,
+                                 void* ws2, size_t ws2_bytes, void* stream2, double tol,
+                                 int max_inner, uint32_t* metric, int mma) {
+  return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
+                   max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2, modes2, ws2,
+                   ws2_bytes, stream2);
 }
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,

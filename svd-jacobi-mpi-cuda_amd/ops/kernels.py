@@ -225,6 +225,33 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             metric[1] += nrot
 
 
+def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native"):
+    """Two independent chains of block steps, staggered (svdj_block_steps2).
+    ``chain_x = (pairs, modes, ws_slot, stream)``: device pairs (steps, P, 2),
+    host modes, a workspace slot and the torch stream of that chain.  Step s
+    of chain b starts when chain a's EVD of step s is done.  On CPU tensors
+    the chains run one after the other."""
+    if not At.is_cuda:
+        for pairs, modes, slot, _ in (chain_a, chain_b):
+            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma)
+        return
+    _check_layout(At, m_pad)
+    check_block(At.dtype, W)
+    args = []
+    for pairs, modes, slot, stream in (chain_a, chain_b):
+        steps, P = int(pairs.shape[0]), int(pairs.shape[1])
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot)
+        md = (C.c_int32 * max(steps, 1))(*[int(x) for x in modes])
+        args.append((_ptr(pairs), P, steps, md, _ptr(ws), ws.numel(),
+                     C.c_void_p(stream.cuda_stream)))
+    n_v = Vt.shape[1] if Vt is not None else 0
+    ldv = Vt.stride(0) if Vt is not None else 0
+    hip_check(hip_lib().svdj_block_steps2(
+        dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
+        *args[0], *args[1], float(tol), int(max_inner), _ptr(metric), mma_code(mma, At.dtype)),
+        "block_steps2")
+
+
 def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
     """Xt (2W, ld) rows = columns of X, in place X <- X Q (device tensors)."""
     _check_layout(Xt, Xt.shape[1] // ROW_ALIGN * ROW_ALIGN)
@@ -272,6 +299,6 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
 __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "dtype_code", "new_metric", "reset_metric",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
-    "block_workspace", "block_steps", "block_solve", "check_block", "MMA_CODES", "mma_code",
+    "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",
 ]

@@ -195,11 +195,18 @@ class DistributedBlockJacobi(Solver):
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma)
+
+            def run_pair(a, b):
+                K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
+                               mma=mma)
+
+            if not cfg.stagger:
+                run_pair = None
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
                 if pipelined:
-                    t_comm += ex.run(splan, run_steps, phys)
+                    t_comm += ex.run(splan, run_steps, phys, run_pair)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:

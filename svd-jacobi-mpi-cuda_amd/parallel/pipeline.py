@@ -109,6 +109,39 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
     return plan
 
 
+def issue_groups(items: list, stagger: bool) -> list:
+    """The plan's items regrouped for issue: a Task, a Send, or a (Task, Task)
+    pair issued jointly as two staggered chains (ops.kernels.block_steps2).
+
+    A task is paired with the next task (at most one Send in between) when the
+    two run on different streams, touch disjoint halves, and the Send in
+    between concerns neither of the second task's halves; that Send is then
+    issued after the pair (it only waits on events of earlier users of its
+    half, so the delay is host-side only).  Pairs: rr0+rr1, T01+T10, and the
+    last round's T00+T11 / T01+T10; T11 of a round pairs with T00 of the next
+    round across the half-1 Send."""
+    out = []
+    i, n = 0, len(items)
+    while i < n:
+        it = items[i]
+        if stagger and isinstance(it, Task):
+            j = i + 1
+            while j < n and isinstance(items[j], Send):
+                j += 1
+            sends = items[i + 1:j]
+            if j < n and len(sends) <= 1:
+                b = items[j]
+                if (b.stream != it.stream and not set(b.halves) & set(it.halves)
+                        and all((x.slot, x.half) not in b.halves for x in sends)):
+                    out.append((it, b))
+                    out.extend(sends)
+                    i = j + 1
+                    continue
+        out.append(it)
+        i += 1
+    return out
+
+
 def check_plan_coverage(plans: list, tour) -> None:
     """Simulate one sweep on every GPU (``plans[g]`` is GPU g's plan; all have
     the same item structure) on global block ids, from the tournament's
@@ -174,6 +207,7 @@ class PipelineExecutor:
                       else None,
                       torch.empty(hB, dtype=D.dtype, device=dev)) for _ in range(2)]
         self.dev_pairs = {}  # item index -> device pairs (the plan is fixed per solve)
+        self._groups = {}
         self.comm_stream = torch.cuda.Stream(dev) if self.cuda and comm.distributed else None
 
     def _rows(self, slot: int, half: int) -> slice:
@@ -187,11 +221,13 @@ class PipelineExecutor:
             self.dev_pairs[i] = t
         return t
 
-    def run(self, plan: SweepPlan, run_steps, phys) -> float:
+    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
-        steps on the current stream.  ``phys`` (per-GPU placement of whole
-        super-blocks) is updated after both halves of a round arrived.
-        Returns host seconds spent issuing/blocking on exchanges."""
+        steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
+        independent chains staggered, ``a``/``b`` = (pairs, modes, slot,
+        stream).  ``phys`` (per-GPU placement of whole super-blocks) is
+        updated after both halves of a round arrived.  Returns host seconds
+        spent issuing/blocking on exchanges."""
         import time
 
         if self.cuda:  # everything enqueued on the caller's stream so far (metric
@@ -204,7 +240,12 @@ class PipelineExecutor:
         pending = {}    # (slot, half) -> (works, buffers) received, not yet copied
         t_comm = 0.0
         halves_done = {}
-        for i, it in enumerate(plan.items):
+        index = {id(it): i for i, it in enumerate(plan.items)}
+        groups = self._groups.get(id(plan))
+        if groups is None:
+            groups = issue_groups(plan.items, run_pair is not None)
+            self._groups[id(plan)] = groups
+        for it in groups:
             if isinstance(it, Send):
                 tc = time.perf_counter()
                 self._send(it, last, pending)
@@ -213,23 +254,33 @@ class PipelineExecutor:
                     self._update_phys(it.round, phys)
                 t_comm += time.perf_counter() - tc
                 continue
-            pairs = self._pairs(i, it)
+            tasks = it if isinstance(it, tuple) else (it,)
+            pairs = [self._pairs(index[id(t)], t) for t in tasks]
             if not self.cuda:
-                for hv in it.halves:
-                    self._consume(hv, pending)
-                run_steps(pairs, it.modes, it.stream)
+                for t, pr in zip(tasks, pairs):
+                    for hv in t.halves:
+                        self._consume(hv, pending)
+                    run_steps(pr, t.modes, t.stream)
                 continue
-            s = self.streams[it.stream]
-            with torch.cuda.stream(s):
-                for hv in it.halves:
-                    for ev in last.get(hv, ()):
-                        s.wait_event(ev)
-                    self._consume(hv, pending)
-                run_steps(pairs, it.modes, it.stream)
+            for t in tasks:  # dependencies, on each task's own stream
+                s = self.streams[t.stream]
+                with torch.cuda.stream(s):
+                    for hv in t.halves:
+                        for ev in last.get(hv, ()):
+                            s.wait_event(ev)
+                        self._consume(hv, pending)
+            if len(tasks) == 2:
+                a, b = tasks
+                run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
+                         (pairs[1], b.modes, b.stream, self.streams[b.stream]))
+            else:
+                with torch.cuda.stream(self.streams[tasks[0].stream]):
+                    run_steps(pairs[0], tasks[0].modes, tasks[0].stream)
+            for t in tasks:
                 ev = torch.cuda.Event()
-                ev.record(s)
-            for hv in it.halves:
-                last.setdefault(hv, []).append(ev)
+                ev.record(self.streams[t.stream])
+                for hv in t.halves:
+                    last.setdefault(hv, []).append(ev)
         if self.cuda:
             main = torch.cuda.current_stream(self.At.device)
             for s in self.streams:

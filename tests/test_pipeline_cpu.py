@@ -38,3 +38,35 @@ def test_sends_follow_last_use():
 def test_odd_k_rejected():
     with pytest.raises(ValueError):
         pipeline.sweep_plan(2, 3, schedule.tournament(2).xslot[:, 0])
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("k", [2, 4, 6])
+def test_stagger_groups_keep_coverage(P, k):
+    """Joint (staggered) issue pairs independent tasks of different streams;
+    the regrouped order (Sends moved after a pair) still meets every pair
+    once and never moves a Send past a task that touches its half."""
+    tour = schedule.tournament(P)
+    plans = [pipeline.sweep_plan(P, k, tour.xslot[:, g]) for g in range(P)]
+    regrouped = []
+    for pl in plans:
+        groups = pipeline.issue_groups(pl.items, True)
+        pos = {id(x): i for i, x in enumerate(pl.items)}
+        flat = []
+        for g in groups:
+            if isinstance(g, tuple):
+                a, b = g
+                assert a.stream != b.stream and not set(a.halves) & set(b.halves)
+                for x in pl.items[pos[id(a)] + 1:pos[id(b)]]:  # Sends moved after the pair
+                    assert isinstance(x, pipeline.Send) and (x.slot, x.half) not in b.halves
+                flat += [a, b]
+            else:
+                flat.append(g)
+        assert sorted(map(id, flat)) == sorted(map(id, pl.items))
+        npairs = sum(isinstance(g, tuple) for g in groups)
+        assert npairs >= (2 * P - 1) + 1 - (1 if P > 1 else 0)
+        new = pipeline.SweepPlan(pl.P, pl.k)
+        new.items = flat
+        regrouped.append(new)
+    pipeline.check_plan_coverage(regrouped, tour)
+    assert pipeline.issue_groups(plans[0].items, False) == plans[0].items
