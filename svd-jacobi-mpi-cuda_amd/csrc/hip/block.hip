@@ -305,6 +305,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   __shared__ RotRec<T> prm[W];
   __shared__ int sweep_rot;
   __shared__ float wmax[NWAVE];
+  __shared__ float pair_max;
 
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
@@ -359,8 +360,17 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       float m2 = 0.0f;
       for (int w = 0; w < NWAVE; ++w) m2 = wmax[w] > m2 ? wmax[w] : m2;
       atomic_max_pos(&metric[0], m2);
+      pair_max = m2;
     }
+    __syncthreads();
   }
+  // Every coupling already below tol: the first Jacobi pass would rotate
+  // nothing (rotations fire on the same |g_pq| / sqrt(g_pp g_qq) > tol test
+  // and nothing else changes G), so skip the pass outright.  Late sweeps are
+  // mostly such pairs, and the final confirming sweep is all of them.
+  // (fp64: a 1e-3 relative margin covers the float rounding of the metric.)
+  const bool converged_pair = sizeof(T) == 4 ? pair_max <= (float)tol
+                                             : pair_max < (float)tol * 0.999f;
 
   // ---- off-diagonal slot-pair blocks (a < b) owned by this thread, dealt
   // round robin (W=64: 2016 blocks -> 2 per thread).  The diagonal blocks
@@ -399,7 +409,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   auto sidx = [](int i, int j) { return i < j ? i * LD + j : j * LD + i; };
 
   bool any = false;
-  for (int sw = 0; sw < max_inner; ++sw) {
+  for (int sw = 0; sw < (converged_pair ? 0 : max_inner); ++sw) {
     for (int st = 0; st < N - 1; ++st) {
       EVD_T(0);
       // (1) wave 0 solves the W rotations of this step and publishes them in

@@ -19,9 +19,12 @@ from .base import SVDResult, Solver, Timer
 def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     if dtype == torch.float64:
         return 32
-    # fp32: W=64 halves the per-byte traffic once there are enough pairs to
-    # fill the chip (>= ~64 pairs per step); small problems prefer W=32.
-    return 64 if n >= 4096 else 32
+    # fp32: W=64 halves the per-byte traffic of the Gram and needs half the
+    # steps, but its EVD is 4.5x slower (280 vs 62 us).  Measured with the
+    # staggered chains (MI355X, n x n, s per solve W=32 / W=64): 2048: 0.087 /
+    # 0.160, 4096: 0.27 / 0.40, 8192: 1.23 / 1.31, 16384: 9.07 / 6.81.  ``n``
+    # is the per-GPU column count (distributed callers pass n / P).
+    return 64 if n >= 12288 else 32
 
 
 class BlockJacobi(Solver):
