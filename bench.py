@@ -165,6 +165,8 @@ def main():
                 "super_block_B": geo["B"],
                 "mma": results[-1].info.get("mma", a.mma),
                 "precondition": results[-1].info.get("precondition", "none"),
+                "chains": a.chains,
+                "staggered": not a.no_stagger,
             },
             "sweeps": sweeps,
             "converged": conv,
