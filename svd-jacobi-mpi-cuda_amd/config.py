@@ -61,6 +61,7 @@ class SolverConfig:
     chains: int = 2                 # block path: independent step chains on separate streams
     stagger: bool = True            # offset the two chains by an EVD (svdj_block_steps2)
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
+    progress: bool = False          # rank 0 prints one line per sweep to stderr
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)

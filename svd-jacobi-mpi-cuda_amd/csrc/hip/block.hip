@@ -216,13 +216,14 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Per-slot rotation record published by wave 0 each step: (c, s) in fp64
-// for the Q accumulation, (c, s, t) in the data precision for G, players.
+// Per-slot rotation published by wave 0 each step, structure of arrays: the
+// (c, s) pairs 2*sizeof(T) apart so the phase-(2) reads of consecutive slots
+// (one per lane) hit consecutive banks (a 32-byte array-of-structs record put
+// 8 lanes on each bank pair: 2-3 extra LDS cycles per read, rocprofv3
+// SQ_LDS_BANK_CONFLICT, profiles/r1_s4_pmc); t in its own array.
 template <typename T>
-struct alignas(16) RotRec {
-  double c64, s64;
-  T c, s, t;
-  int pq;  // p | q << 16
+struct alignas(2 * sizeof(T)) CSPair {
+  T c, s;
 };
 
 // Fast fp32 rotation (raw v_sqrt/v_rcp/v_rsq, ~1 ulp): only steers G; Q is
@@ -302,7 +303,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   static_assert(N % NGRP == 0, "rows must split evenly over row groups");
 
   __shared__ T G[N * LD];
-  __shared__ RotRec<T> prm[W];
+  __shared__ CSPair<T> prm_cs[W];
+  __shared__ T prm_t[W];
   __shared__ int sweep_rot;
   __shared__ float wmax[NWAVE];
   __shared__ float pair_max;
@@ -386,9 +388,17 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     const int idx = tid + j * NT;
     ba[j] = bb[j] = -1;
     if (idx < NOFF) {
-      // idx -> (a, b), a < b, row-major over the strict upper triangle
-      int a = 0, base = 0;
-      while (idx >= base + (W - 1 - a)) { base += W - 1 - a; ++a; }
+      // idx -> (a, b), a < b, over the strict upper triangle in rows taken
+      // in complementary pairs 0, W-2, 1, W-3, ...: a pair of rows is W blocks,
+      // so a 32-lane LDS group spans fewer row boundaries, where G's bank
+      // (p + r) mod 32 repeats (host simulation of all steps: 0.9 vs 1.5
+      // extra LDS cycles per G access at W=32, 0.6 vs 0.9 at W=64)
+      int i = 0, base = 0, a = 0;
+      for (;; ++i) {
+        a = (i & 1) ? W - 2 - (i >> 1) : (i >> 1);
+        if (idx < base + (W - 1 - a)) break;
+        base += W - 1 - a;
+      }
       ba[j] = a;
       bb[j] = a + 1 + (idx - base);
     }
@@ -419,7 +429,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         const int ipq = sidx(pf, ps);
         const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[ipq];
         T c = 1, s = 0, t = 0;
-        RotRec<T> r;
         if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) {
           sweep_rot = 1;
           // this slot's diagonal block (exact update)
@@ -427,13 +436,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
           G[ps * LD + ps] = gqq + t * gpq;
           G[ipq] = T(0);
         }
-        r.c64 = 0.0;
-        r.s64 = 0.0;
-        r.c = c;
-        r.s = s;
-        r.t = t;
-        r.pq = pf | (ps << 16);
-        prm[slot] = r;
+        prm_cs[slot] = CSPair<T>{c, s};
+        prm_t[slot] = t;
       }
       EVD_T(1);
       __syncthreads();
@@ -448,7 +452,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         ring_slot<W>(bb[j], st, r, u);
         const int i00 = sidx(p, r), i01 = sidx(p, u), i10 = sidx(q, r), i11 = sidx(q, u);
         const T g00 = G[i00], g01 = G[i01], g10 = G[i10], g11 = G[i11];
-        const T ca = prm[ba[j]].c, sa = prm[ba[j]].s, cb = prm[bb[j]].c, sb = prm[bb[j]].s;
+        const CSPair<T> ra = prm_cs[ba[j]], rb = prm_cs[bb[j]];
+        const T ca = ra.c, sa = ra.s, cb = rb.c, sb = rb.s;
         const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
         const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
         G[i00] = cb * h00 - sb * h01;
@@ -458,12 +463,12 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       }
       // (3) Q <- Q J in registers (fp64): (c, s) from t, normalised in fp64
       {
-        const T tq = prm[slot].t;
+        const T tq = prm_t[slot];
         if (tq != T(0)) {
           double c64, s64;
           if constexpr (sizeof(T) == 8) {
-            c64 = prm[slot].c;
-            s64 = prm[slot].s;
+            c64 = prm_cs[slot].c;
+            s64 = prm_cs[slot].s;
           } else {
             const double td = (double)tq;
             c64 = rsqrt64(1.0 + td * td);

@@ -27,6 +27,7 @@ reference's layout, or left distributed.
 """
 from __future__ import annotations
 
+import sys
 import time
 
 import torch
@@ -221,6 +222,9 @@ class DistributedBlockJacobi(Solver):
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
+            if cfg.progress and g == 0:
+                print(f"[svdj] sweep {sweeps}: off {mx:.3e}, rotated pairs {nrot}, "
+                      f"{time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
             if nrot == 0:
                 converged = True
                 break
