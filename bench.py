@@ -12,6 +12,18 @@ n(n-1)/2 * (12 m + 6 n), times the sweeps actually
 executed, divided by the measured wall time of the solve; the value is the
 whole-job aggregate.  Strong scaling: the matrix size is fixed as N grows.
 
+Input/output placement:
+  default       every rank generates its own columns inside the timed region
+                (on-the-fly input) and keeps its U/V/sigma columns;
+  --root-owned  rank 0 holds A before the timed region; the timed region
+                includes the scatter to all ranks and the gather of U, sigma
+                and V back to rank 0 (the reference's timing, main.cu:1586-1611).
+
+Simulation (one process, no RCCL): ``--simulate-P P --simulate-rank g`` runs
+rank g's exact per-GPU plan of a P-GPU job with every exchange replaced by a
+device swap of the real message sizes (parallel/comm.py SimCommunicator), for
+a fixed number of sweeps; it reports the per-GPU time per sweep.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16384]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
@@ -67,6 +79,91 @@ def verify_distributed(res, gen, m, n, comm, dtype):
             "orth_u_blockdiag_fro": float(parts[3].sqrt())}
 
 
+def verify_root(res, A, dtype):
+    """Rank 0, root-owned output: full ||A V - U S|| / ||A|| and orthogonality."""
+    U, S, V = res.U.to(dtype), res.S.to(dtype), res.V.to(dtype)
+    A = A.to(dtype)
+    eye = torch.eye(S.shape[0], device=A.device, dtype=dtype)
+    r = (A @ V - U * S).double().norm() / A.double().norm()
+    return {"residual_rel": float(r),
+            "orth_v_fro": float((V.t() @ V - eye).double().norm()),
+            "orth_u_fro": float((U.t() @ U - eye).double().norm())}
+
+
+def make_generator(m, dev, work, dtype):
+    GB = 256  # generator block: the matrix is fixed regardless of how callers chunk it
+
+    def gen(c0, c1):  # synthetic random dense U(0,1), columns c0..c1-1 of ONE fixed matrix
+        parts = []
+        for b0 in range(c0 // GB * GB, c1, GB):
+            g = torch.Generator(device=dev).manual_seed(1234 + b0)
+            blk = torch.rand(m, GB, generator=g, dtype=work, device=dev)
+            parts.append(blk[:, max(c0 - b0, 0):min(c1 - b0, GB)])
+        return torch.cat(parts, dim=1).to(dtype)
+
+    return gen
+
+
+def simulate(a, cfg, dtype, work):
+    """Per-GPU time of rank g's plan in a P-GPU job, on one GPU."""
+    import svdj
+    from svdj.parallel import DistributedBlockJacobi, SimCommunicator
+    from svdj.utils.layout import pad_rows
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    P, g = a.simulate_P, a.simulate_rank
+    n = a.n
+    m = a.m or n
+    m_pad = pad_rows(m)
+    gen = make_generator(m, dev, work, dtype)
+    seed_gen = torch.Generator(device=dev).manual_seed(99)
+    made = []
+
+    def seed(pos, like):  # other ranks' super-block halves: [A half, D half, V half]
+        if pos == 0:
+            t = torch.zeros_like(like)
+            t[:, :m] = torch.rand(like.shape[0], m, generator=seed_gen, device=dev,
+                                  dtype=work).to(like.dtype)
+            made.append(t)
+            return t
+        if pos == 1:  # squared norms of the matching A half
+            return made.pop(0).double().pow(2).sum(1).to(like.dtype)
+        return torch.zeros_like(like)
+
+    comm = SimCommunicator(P, g, dev, seed_fn=seed, link_gbps=a.sim_link_gbps)
+    cfg.max_sweeps = a.sim_sweeps
+    cfg.comm_timing = True
+    solver = DistributedBlockJacobi(cfg, comm)
+
+    def one():
+        return solver.solve(None, m=m, n=n, dtype=dtype, generator=gen, gather=False)
+
+    one()  # warmup (compiles nothing; allocates workspaces and the ring)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    geo = res.info["geometry"]
+    line = {
+        "metric": "simulated per-GPU time per sweep (rank plan of a P-GPU job on one GPU)",
+        "value": round(el / res.sweeps * 1e3, 3), "unit": "ms/sweep", "higher_is_better": False,
+        "simulated_P": P, "simulated_rank": g, "sweeps_run": res.sweeps,
+        "solve_s": round(el, 4), "dtype": a.dtype,
+        "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
+                   "chains": a.chains, "link_gbps_model": a.sim_link_gbps},
+        "comm": res.info.get("comm"),
+        "sim_bytes_per_exchange": comm.bytes_moved // max(comm.exchanges, 1),
+        "note": "exchanges swap with simulated peers (device copies of the real sizes); "
+                "numerics are not those of the real job -- timing only",
+    }
+    print(json.dumps(line), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(line, f)
+
+
 def main():
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument("--gpus", type=int, default=1)
@@ -86,6 +183,16 @@ def main():
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
                    help="block apply matrix cores (auto = native f32/f64 MFMA; bf16x6/bf16x3 "
                         "split modes are faster but not fp32-accurate on every input)")
+    p.add_argument("--root-owned", action="store_true",
+                   help="A on rank 0 before timing; scatter + gather of U,S,V timed")
+    p.add_argument("--progress", action="store_true", help="one line per sweep on stderr")
+    p.add_argument("--comm-timeout", type=float, default=None,
+                   help="process-group timeout in s (default SVDJ_COMM_TIMEOUT or 600)")
+    p.add_argument("--simulate-P", type=int, default=0)
+    p.add_argument("--simulate-rank", type=int, default=0)
+    p.add_argument("--sim-sweeps", type=int, default=3)
+    p.add_argument("--sim-link-gbps", type=float, default=0.0,
+                   help="model each exchange's link time at this GB/s (0: device copy only)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--no-verify", action="store_true",
                    help="skip the post-timing accuracy check")
@@ -94,35 +201,36 @@ def main():
     import svdj
     from svdj.parallel import Communicator, DistributedBlockJacobi
 
+    dtype = {"fp32": torch.float32, "fp64": torch.float64, "bf16": torch.bfloat16}[a.dtype]
+    work = torch.float64 if dtype == torch.float64 else torch.float32
+    cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
+                            max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
+                            stagger=not a.no_stagger, precondition=a.precondition,
+                            progress=a.progress, comm_timing=a.gpus > 1)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    if a.simulate_P:
+        simulate(a, cfg, dtype, work)
+        return
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with "
                          "torch.distributed.run --nproc-per-node N")
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU")
-    comm = Communicator()
-    dtype = {"fp32": torch.float32, "fp64": torch.float64, "bf16": torch.bfloat16}[a.dtype]
-    work = torch.float64 if dtype == torch.float64 else torch.float32
-    n = a.n
-    m = a.m or n
-    cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
-                            max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
-                            stagger=not a.no_stagger,
-                            precondition=a.precondition)
+    comm = Communicator(timeout_s=a.comm_timeout)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
+    n = a.n
+    m = a.m or n
+    gen = make_generator(m, dev, work, dtype)
 
-    GB = 256  # generator block: the matrix is fixed regardless of how callers chunk it
-
-    def gen(c0, c1):  # synthetic random dense U(0,1), columns c0..c1-1 of ONE fixed matrix
-        parts = []
-        for b0 in range(c0 // GB * GB, c1, GB):
-            g = torch.Generator(device=dev).manual_seed(1234 + b0)
-            blk = torch.rand(m, GB, generator=g, dtype=work, device=dev)
-            parts.append(blk[:, max(c0 - b0, 0):min(c1 - b0, GB)])
-        return torch.cat(parts, dim=1).to(dtype)
+    A_root = None
+    if a.root_owned and comm.rank == 0:
+        A_root = gen(0, n)
 
     def one():
+        if a.root_owned:
+            return solver.solve(A_root if comm.rank == 0 else None, gather=True)
         return solver.solve(None, m=m, n=n, dtype=dtype, generator=gen, gather=False)
 
     for _ in range(a.warmup):
@@ -130,18 +238,28 @@ def main():
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = [one() for _ in range(a.steps)]
+    # Only the last solve's outputs are kept (earlier ones are released as the
+    # next solve starts); sweeps / convergence / flops are accumulated as scalars.
+    sweeps, conv, flops, last = [], True, 0.0, None
+    for _ in range(a.steps):
+        last = None
+        last = one()
+        sweeps.append(last.sweeps)
+        conv = conv and last.converged
+        flops += last.info["flops"]
     comm.barrier()
     torch.cuda.synchronize()
     elapsed = comm.max_over_ranks(time.perf_counter() - t0)
 
-    sweeps = [r.sweeps for r in results]
-    conv = all(r.converged for r in results)
-    flops = sum(r.info["flops"] for r in results)
     gflops = flops / elapsed / 1e9
     ms = elapsed / a.steps * 1e3
-    geo = results[-1].info["geometry"]
-    acc = None if a.no_verify else verify_distributed(results[-1], gen, m, n, comm, work)
+    geo = last.info["geometry"]
+    acc = None
+    if not a.no_verify:
+        if a.root_owned:
+            acc = verify_root(last, A_root, work) if comm.rank == 0 else None
+        else:
+            acc = verify_distributed(last, gen, m, n, comm, work)
     if comm.rank == 0:
         line = {
             "metric": BASELINE_METRIC,
@@ -155,7 +273,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic random dense U(0,1), seeded per column block",
+            "data": "synthetic random dense U(0,1), seeded per column block" +
+                    ("; root-owned A, scatter+gather timed" if a.root_owned
+                     else "; generated on the fly per rank"),
             "config": {
                 "model": f"{m}x{n} {a.dtype} block one-sided Jacobi SVD (AllVec), to convergence",
                 "global_batch": 1,
@@ -163,16 +283,17 @@ def main():
                 "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                 "block_W": geo["W"],
                 "super_block_B": geo["B"],
-                "mma": results[-1].info.get("mma", a.mma),
-                "precondition": results[-1].info.get("precondition", "none"),
+                "mma": last.info.get("mma", a.mma),
+                "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
                 "staggered": not a.no_stagger,
+                "root_owned": a.root_owned,
             },
             "sweeps": sweeps,
             "converged": conv,
             "time_to_converge_s": round(ms / 1e3, 4),
-            "off_history_last": [float("%.3e" % h) for h in results[-1].history[-3:]],
-            "comm_seconds_rank0": round(results[-1].info["comm_seconds"], 4),
+            "off_history_last": [float("%.3e" % h) for h in last.history[-3:]],
+            "comm": last.info.get("comm"),
             "accuracy": acc,
         }
         print(json.dumps(line), flush=True)

@@ -62,6 +62,7 @@ class SolverConfig:
     stagger: bool = True            # offset the two chains by an EVD (svdj_block_steps2)
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     progress: bool = False          # rank 0 prints one line per sweep to stderr
+    comm_timing: bool = False       # distributed: HIP-event timing of every exchange
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
@@ -110,6 +111,7 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--precondition", default="auto", choices=["auto", "qr", "none"])
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
+    p.add_argument("--progress", action="store_true", help="print one line per sweep (rank 0)")
     return p
 
 
@@ -118,4 +120,5 @@ def config_from_args(a) -> SolverConfig:
                         block=a.block, tol=a.tol, tol_mode=a.tol_mode, max_sweeps=a.max_sweeps,
                         max_inner_sweeps=a.max_inner_sweeps, ordering=a.ordering, sort=a.sort,
                         mma=a.mma, precondition=a.precondition, checkpoint_dir=a.checkpoint_dir,
-                        checkpoint_every=a.checkpoint_every)
+                        checkpoint_every=a.checkpoint_every,
+                        progress=bool(getattr(a, "progress", False)))

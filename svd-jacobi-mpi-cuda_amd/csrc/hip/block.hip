@@ -25,6 +25,7 @@
 #include "svdj_hip.h"
 
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 namespace svdj {
@@ -156,41 +157,32 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
 }
 
 // -------------------------------------------------------------------- evd
-// Round-robin (circle) pairing of N indices, step st, slot a.
-__device__ __forceinline__ void rr_pair(int st, int a, int N, int& p, int& q) {
-  if (a == 0) {
-    p = st;
-    q = N - 1;
-  } else {
-    p = (st + a) % (N - 1);
-    q = (st - a + N - 1) % (N - 1);
-  }
-  if (p > q) {
-    int t = p;
-    p = q;
-    q = t;
-  }
-}
-
-// The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair:
-//   * G lives in LDS (data precision, upper triangle maintained, indexed by
-//     column id), updated per parallel step as independent 2x2 blocks
-//     (J_a^T G J_b) -- every entry belongs to exactly one block, and each
-//     thread owns a fixed set of slot-pair blocks for the whole kernel;
-//   * the rotation accumulator Q lives in REGISTERS, always in fp64, in
-//     "slot layout": lane (slot a, row group g) holds Q[k][first(a)] and
-//     Q[k][second(a)] for its rows k.  The circle-method round robin moves
-//     one player per slot to the neighbouring slot each step, which is a
-//     one-lane DPP shift (wave_shr:1 / wave_shl:1) -- no LDS traffic for Q.
-//     fp64 accumulation keeps Q orthogonal to ~1e-16 before it is rounded to
-//     the data type, so V stays orthogonal over hundreds of block steps;
-//   * per step: every lane solves its slot's rotation in the data precision
-//     (fp32 for fp32 data), one lane per slot publishes (c, s, t, p|q) as one
-//     16/32-byte record, barrier, then G blocks are updated from the records
-//     while the fp64 (c, s) for Q are formed from t off the critical path
-//     (c^2 + s^2 = 1 to fp64 accuracy), barrier, DPP shift.
+// The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair, as a
+// cyclic parallel Jacobi (circle-method round robin: W disjoint rotations per
+// step, 2W-1 steps per sweep):
+//   * G lives in LDS (data precision, upper triangle, indexed by player id);
+//     every off-diagonal slot-pair block (a < b) of a step is owned by one
+//     thread for the whole kernel (the blocks are dealt once);
+//   * ONE barrier per step.  The rotations of step st+1 are solved inside
+//     step st's update phase: the coupling g_xy of a next-step pair (x, y)
+//     lies in exactly one off-diagonal block of step st (x and y sit in
+//     different slots there), so the thread owning that block computes the
+//     new g_xy, takes the post-step diagonals of x and y from the step-st
+//     rotation records, solves step st+1's rotation right away and publishes
+//     it (c, s, t and the post-rotation diagonals) into the other half of a
+//     double-buffered record array.  The reference solves every 2x2 on the
+//     host between two kernel launches (main.cu:698-725); the previous kernel
+//     here still needed a solve phase and a second barrier per step;
+//   * the rotation accumulator Q lives in REGISTERS in fp64, in "slot layout":
+//     lane (slot a, row group g) holds Q[k][first(a)] and Q[k][second(a)] for
+//     its rows k.  The circle-method movement is a one-lane DPP shift per step
+//     (wave_shr:1 / wave_shl:1); fp64 keeps Q orthogonal to ~1e-16 before it
+//     is rounded to the data type, so V stays orthogonal over hundreds of
+//     block steps;
+//   * the diagonal never lives in G after the start: it travels in the
+//     records (a rotation of slot a changes only d_first and d_second).
 #ifndef SVDJ_EVD_THREADS_32
-#define SVDJ_EVD_THREADS_32 1024  // measured: 64 us vs 78 us (512) per W=32 EVD
+#define SVDJ_EVD_THREADS_32 512
 #endif
 #ifndef SVDJ_EVD_THREADS_64
 #define SVDJ_EVD_THREADS_64 1024
@@ -216,22 +208,28 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Per-slot rotation published by wave 0 each step, structure of arrays: the
-// (c, s) pairs 2*sizeof(T) apart so the phase-(2) reads of consecutive slots
-// (one per lane) hit consecutive banks (a 32-byte array-of-structs record put
-// 8 lanes on each bank pair: 2-3 extra LDS cycles per read, rocprofv3
-// SQ_LDS_BANK_CONFLICT, profiles/r1_s4_pmc); t in its own array.
-template <typename T>
-struct alignas(2 * sizeof(T)) CSPair {
-  T c, s;
-};
+// Rotation test, shared by the solve and the "nothing to do" pre-pass so the
+// two decide identically: relative |g_pq| > tol sqrt(g_pp g_qq) (fp32: raw
+// v_sqrt, ~1 ulp), or the reference's absolute |g_pq| > tol (TOLERANCE,
+// reference lib/global.cuh:9, main.cu:714) when absmode.
+__device__ __forceinline__ bool needs_rotation(float gpp, float gqq, float gpq, float tol,
+                                               int absmode) {
+  if (absmode) return fabsf(gpq) > tol;
+  const float nrm = __builtin_amdgcn_sqrtf(gpp) * __builtin_amdgcn_sqrtf(gqq);
+  return nrm > 0.0f && fabsf(gpq) > tol * nrm;
+}
+__device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gpq, double tol,
+                                               int absmode) {
+  if (absmode) return fabs(gpq) > tol;
+  const double nrm = sqrt(gpp) * sqrt(gqq);
+  return nrm > 0.0 && fabs(gpq) > tol * nrm;
+}
 
 // Fast fp32 rotation (raw v_sqrt/v_rcp/v_rsq, ~1 ulp): only steers G; Q is
-// built from the fp64-normalised (c, s).
+// built from the fp64-normalised (c, s) of t.
 __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, float tol,
-                                              float& c, float& s, float& t) {
-  const float nrm = __builtin_amdgcn_sqrtf(gpp) * __builtin_amdgcn_sqrtf(gqq);
-  if (!(nrm > 0.0f) || !(fabsf(gpq) > tol * nrm)) return false;
+                                              int absmode, float& c, float& s, float& t) {
+  if (!needs_rotation(gpp, gqq, gpq, tol, absmode)) return false;
   const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * gpq);
   const float at = fabsf(tau);
   float tt = at > 1e18f ? 0.5f * __builtin_amdgcn_rcpf(at)
@@ -242,9 +240,8 @@ __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, f
   return true;
 }
 __device__ __forceinline__ bool rotation_fast(double gpp, double gqq, double gpq, double tol,
-                                              double& c, double& s, double& t) {
-  const double nrm = sqrt(gpp) * sqrt(gqq);
-  if (!(nrm > 0.0) || !(fabs(gpq) > tol * nrm)) return false;
+                                              int absmode, double& c, double& s, double& t) {
+  if (!needs_rotation(gpp, gqq, gpq, tol, absmode)) return false;
   schur_rotation<double>(gpq, gpp, gqq, c, s, t);
   return true;
 }
@@ -268,11 +265,11 @@ __device__ unsigned long long g_evd_prof[16];
 #endif
 
 // Circle-method players of slot a at step st (the same movement as the DPP
-// shifts of the register Q below: firsts move right, seconds left, player
-// N-1 fixed in slot 0).  Ring of N-1 positions; slot a >= 1 has its first at
+// shifts of the register Q: firsts move right, seconds left, player N-1 fixed
+// in slot 0).  Ring of R = N-1 positions; slot a >= 1 has its first at
 // position a-1 and its second at 2W-2-a; the player at position x after st
-// steps is ((x - st) mod (N-1) + 1) mod (N-1).  Checked against the DPP
-// movement by tests/test_schedule.py::test_evd_ring_matches_dpp_movement.
+// steps is ((x - st) mod R + 1) mod R.  Checked against the DPP movement by
+// tests/test_schedule.py::test_evd_ring_matches_dpp_movement.
 template <int W>
 __device__ __forceinline__ int ring_player(int pos, int st) {
   constexpr int R = 2 * W - 1;
@@ -285,101 +282,120 @@ __device__ __forceinline__ void ring_slot(int a, int st, int& p, int& q) {
   p = a == 0 ? 2 * W - 1 : ring_player<W>(a - 1, st);
   q = ring_player<W>(2 * W - 2 - a, st);
 }
+// Inverse: slot of player x at step st (0 <= st < R), and whether x is the
+// slot's first.  Encoded as 2*slot + first.
+template <int W>
+__device__ __forceinline__ int ring_where(int x, int st) {
+  constexpr int R = 2 * W - 1;
+  if (x == 2 * W - 1) return 1;  // slot 0, first
+  int pos = (x == 0 ? R - 1 : x - 1) + st;
+  pos -= pos >= R ? R : 0;
+  return pos <= W - 2 ? 2 * (pos + 1) + 1 : 2 * (2 * W - 2 - pos);
+}
 
 template <typename T, int W>
 __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     const int32_t* __restrict__ pairs, int full, const T* __restrict__ slabs, int nchunk,
-    T* __restrict__ D, T* __restrict__ Qout, int32_t* __restrict__ skip, T tol,
+    T* __restrict__ D, T* __restrict__ Qout, int32_t* __restrict__ skip, T tol, int absmode,
     int max_inner, uint32_t* __restrict__ metric) {
   constexpr int NT = evd_threads(W);
   constexpr int NWAVE = NT / SVDJ_WAVE;
   constexpr int N = 2 * W;
+  constexpr int R = N - 1;              // steps per sweep
   constexpr int LD = N + 1;
   constexpr int GPW = SVDJ_WAVE / W;    // row groups per wave
   constexpr int NGRP = NWAVE * GPW;     // row groups
   constexpr int RPL = N / NGRP;         // Q rows per lane
-  constexpr int NBLK = W * (W + 1) / 2; // upper-triangle 2x2 blocks per step
-  constexpr int MAXB = (NBLK + NT - 1) / NT;
   static_assert(N % NGRP == 0, "rows must split evenly over row groups");
 
   __shared__ T G[N * LD];
-  __shared__ CSPair<T> prm_cs[W];
-  __shared__ T prm_t[W];
-  __shared__ int sweep_rot;
+  // rotation records, double-buffered by global step parity (structure of
+  // arrays: consecutive slots on consecutive banks)
+  __shared__ T rc[2][W], rs[2][W], rt[2][W], rdp[2][W], rdq[2][W];
+  __shared__ int rot_flag[2];  // any rotation in sweep (parity)
   __shared__ float wmax[NWAVE];
+  __shared__ int wneed[NWAVE];
   __shared__ float pair_max;
+  __shared__ int need_any;
 
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // ---- assemble G (full symmetric storage)
+  // ---- assemble G (split-K slabs summed in fp64, then rounded once)
   if (full) {
     const T* s0 = slabs + (size_t)pair * nchunk * (4 * W * W);
     for (int i = tid; i < N * N; i += NT) {
-      T acc = 0;
+      double acc = 0;
 #pragma unroll 4
-      for (int c = 0; c < nchunk; ++c) acc += s0[(size_t)c * 4 * W * W + i];
-      G[(i / N) * LD + (i % N)] = acc;
+      for (int c = 0; c < nchunk; ++c) acc += (double)s0[(size_t)c * 4 * W * W + i];
+      G[(i / N) * LD + (i % N)] = (T)acc;
     }
   } else {
     const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
     for (int i = tid; i < N * N; i += NT) G[(i / N) * LD + (i % N)] = T(0);
     __syncthreads();
     for (int i = tid; i < W * W; i += NT) {
-      T acc = 0;
+      double acc = 0;
 #pragma unroll 4
-      for (int c = 0; c < nchunk; ++c) acc += s0[(size_t)c * W * W + i];
+      for (int c = 0; c < nchunk; ++c) acc += (double)s0[(size_t)c * W * W + i];
       const int a = i / W, b = i % W;
-      G[a * LD + W + b] = acc;
-      G[(W + b) * LD + a] = acc;
+      G[a * LD + W + b] = (T)acc;
+      G[(W + b) * LD + a] = (T)acc;
     }
     for (int a = tid; a < W; a += NT) {
       G[a * LD + a] = D[bi * W + a];
       G[(W + a) * LD + W + a] = D[bj * W + a];
     }
   }
-  if (tid == 0) sweep_rot = 0;
+  if (tid == 0) rot_flag[0] = rot_flag[1] = 0;
   __syncthreads();
 
-  // ---- convergence value before any rotation
+  // ---- convergence value before any rotation, and whether any pair would
+  // rotate at all (same test as the solve: if none does, the first pass
+  // rotates nothing -- G never changes -- so it is skipped exactly)
   {
     float mx = 0.0f;
+    int need = 0;
     for (int i = tid; i < N * N; i += NT) {
       const int r = i / N, c = i % N;
       const bool use = full ? (r < c) : (r < W && c >= W);
       if (!use) continue;
-      const T d = sqrt(G[r * LD + r]) * sqrt(G[c * LD + c]);
+      const T grr = G[r * LD + r], gcc = G[c * LD + c], grc = G[r * LD + c];
+      const T d = sqrt(grr) * sqrt(gcc);
       if (d > T(0)) {
-        const float v = (float)(fabs(G[r * LD + c]) / d);
+        const float v = (float)(fabs(grc) / d);
         mx = v > mx ? v : mx;
       }
+      need |= needs_rotation(grr, gcc, grc, tol, absmode) ? 1 : 0;
     }
     mx = wave_max(mx);
-    if (lane == 0) wmax[wave] = mx;
+    need = __any(need) ? 1 : 0;
+    if (lane == 0) {
+      wmax[wave] = mx;
+      wneed[wave] = need;
+    }
     __syncthreads();
     if (tid == 0) {
       float m2 = 0.0f;
-      for (int w = 0; w < NWAVE; ++w) m2 = wmax[w] > m2 ? wmax[w] : m2;
+      int n2 = 0;
+      for (int w = 0; w < NWAVE; ++w) {
+        m2 = wmax[w] > m2 ? wmax[w] : m2;
+        n2 |= wneed[w];
+      }
       atomic_max_pos(&metric[0], m2);
       pair_max = m2;
+      need_any = n2;
     }
     __syncthreads();
   }
-  // Every coupling already below tol: the first Jacobi pass would rotate
-  // nothing (rotations fire on the same |g_pq| / sqrt(g_pp g_qq) > tol test
-  // and nothing else changes G), so skip the pass outright.  Late sweeps are
-  // mostly such pairs, and the final confirming sweep is all of them.
-  // (fp64: a 1e-3 relative margin covers the float rounding of the metric.)
-  const bool converged_pair = sizeof(T) == 4 ? pair_max <= (float)tol
-                                             : pair_max < (float)tol * 0.999f;
+  const bool run = need_any != 0;
 
   // ---- off-diagonal slot-pair blocks (a < b) owned by this thread, dealt
-  // round robin (W=64: 2016 blocks -> 2 per thread).  The diagonal blocks
-  // are updated by wave 0 in phase (1): they hold exactly the three entries
-  // the rotation solve reads, and no off-diagonal block touches them.  (As a
-  // separate unit on the last wave's spare lanes they diverged from the
-  // off-diagonal path: ~3700 cycles/step in that wave vs ~1700 elsewhere.)
+  // round robin over the strict upper triangle in rows taken in
+  // complementary pairs 0, W-2, 1, W-3, ...: a pair of rows is W blocks, so
+  // a 32-lane LDS group spans fewer row boundaries, where G's bank
+  // (p + r) mod 32 repeats.
   constexpr int NOFF = W * (W - 1) / 2;
   constexpr int MAXOFF = (NOFF + NT - 1) / NT;
   int ba[MAXOFF], bb[MAXOFF];
@@ -388,11 +404,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     const int idx = tid + j * NT;
     ba[j] = bb[j] = -1;
     if (idx < NOFF) {
-      // idx -> (a, b), a < b, over the strict upper triangle in rows taken
-      // in complementary pairs 0, W-2, 1, W-3, ...: a pair of rows is W blocks,
-      // so a 32-lane LDS group spans fewer row boundaries, where G's bank
-      // (p + r) mod 32 repeats (host simulation of all steps: 0.9 vs 1.5
-      // extra LDS cycles per G access at W=32, 0.6 vs 0.9 at W=64)
       int i = 0, base = 0, a = 0;
       for (;; ++i) {
         a = (i & 1) ? W - 2 - (i >> 1) : (i >> 1);
@@ -404,7 +415,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     }
   }
 
-  // ---- slot layout state
+  // ---- slot layout state of the register Q
   const int slot = lane % W;
   const int grp = wave * GPW + lane / W;
   int pf = slot == 0 ? N - 1 : slot;          // first player of this slot
@@ -418,57 +429,89 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
   auto sidx = [](int i, int j) { return i < j ? i * LD + j : j * LD + i; };
 
+  // ---- prologue: the rotations of step 0 from the assembled G
+  if (run && tid < W) {
+    int p, q;
+    ring_slot<W>(tid, 0, p, q);
+    const int ipq = sidx(p, q);
+    const T gpp = G[p * LD + p], gqq = G[q * LD + q], gpq = G[ipq];
+    T c = 1, s = 0, t = 0, dp = gpp, dq = gqq;
+    if (rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t)) {
+      dp = gpp - t * gpq;
+      dq = gqq + t * gpq;
+      G[ipq] = T(0);
+      rot_flag[0] = 1;
+    }
+    rc[0][tid] = c;
+    rs[0][tid] = s;
+    rt[0][tid] = t;
+    rdp[0][tid] = dp;
+    rdq[0][tid] = dq;
+  }
+  __syncthreads();
+
   bool any = false;
-  for (int sw = 0; sw < (converged_pair ? 0 : max_inner); ++sw) {
-    for (int st = 0; st < N - 1; ++st) {
+  int gs = 0;  // global step counter: records of step gs live in buffer gs & 1
+  for (int sw = 0; sw < (run ? max_inner : 0); ++sw) {
+    for (int st = 0; st < R; ++st, ++gs) {
       EVD_T(0);
-      // (1) wave 0 solves the W rotations of this step and publishes them in
-      //     the data precision only (the fp64 form for Q is derived per lane
-      //     from t in (3), off this latency-critical single-wave phase)
-      if (wave == 0 && lane < W) {
-        const int ipq = sidx(pf, ps);
-        const T gpp = G[pf * LD + pf], gqq = G[ps * LD + ps], gpq = G[ipq];
-        T c = 1, s = 0, t = 0;
-        if (rotation_fast(gpp, gqq, gpq, tol, c, s, t)) {
-          sweep_rot = 1;
-          // this slot's diagonal block (exact update)
-          G[pf * LD + pf] = gpp - t * gpq;
-          G[ps * LD + ps] = gqq + t * gpq;
-          G[ipq] = T(0);
-        }
-        prm_cs[slot] = CSPair<T>{c, s};
-        prm_t[slot] = t;
-      }
-      EVD_T(1);
-      __syncthreads();
-      EVD_T(2);
-      // (2) G <- J^T G J on this thread's blocks.  Players come from the ring
-      //     formula, so the G loads do not wait for the rotation records.
+      const int b = gs & 1, nb = b ^ 1;
+      const int stn = st + 1 == R ? 0 : st + 1;      // next step (of this or the next sweep)
+      const int nflag = (st + 1 == R ? sw + 1 : sw) & 1;
+      if (sw >= 1 && st == 1 && tid == 0) rot_flag[(sw + 1) & 1] = 0;  // read by all by now
+      // G <- J^T G J on this thread's blocks, and the next step's solves
 #pragma unroll
       for (int j = 0; j < MAXOFF; ++j) {
         if (ba[j] < 0) continue;
         int p, q, r, u;
         ring_slot<W>(ba[j], st, p, q);
         ring_slot<W>(bb[j], st, r, u);
-        const int i00 = sidx(p, r), i01 = sidx(p, u), i10 = sidx(q, r), i11 = sidx(q, u);
-        const T g00 = G[i00], g01 = G[i01], g10 = G[i10], g11 = G[i11];
-        const CSPair<T> ra = prm_cs[ba[j]], rb = prm_cs[bb[j]];
-        const T ca = ra.c, sa = ra.s, cb = rb.c, sb = rb.s;
+        const int idx[4] = {sidx(p, r), sidx(p, u), sidx(q, r), sidx(q, u)};
+        const T g00 = G[idx[0]], g01 = G[idx[1]], g10 = G[idx[2]], g11 = G[idx[3]];
+        const T ca = rc[b][ba[j]], sa = rs[b][ba[j]], cb = rc[b][bb[j]], sb = rs[b][bb[j]];
         const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
         const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
-        G[i00] = cb * h00 - sb * h01;
-        G[i01] = sb * h00 + cb * h01;
-        G[i10] = cb * h10 - sb * h11;
-        G[i11] = sb * h10 + cb * h11;
+        T h[4] = {cb * h00 - sb * h01, sb * h00 + cb * h01, cb * h10 - sb * h11,
+                  sb * h10 + cb * h11};
+        // next-step placement of the four players
+        const int wp = ring_where<W>(p, stn), wq = ring_where<W>(q, stn);
+        const int wr = ring_where<W>(r, stn), wu = ring_where<W>(u, stn);
+        const int wx[4] = {wp, wp, wq, wq}, wy[4] = {wr, wu, wr, wu};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if ((wx[e] >> 1) == (wy[e] >> 1)) {
+            // (x, y) rotate together next step: x from slot ba (role by e>>1),
+            // y from slot bb (role by e&1); post-step-st diagonals from the records
+            const T dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
+            const T dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
+            const bool x_first = wx[e] & 1;
+            const T df = x_first ? dx : dy, ds = x_first ? dy : dx;
+            const int ns = wx[e] >> 1;
+            T c = 1, s = 0, t = 0, dfp = df, dsp = ds;
+            if (rotation_fast(df, ds, h[e], tol, absmode, c, s, t)) {
+              dfp = df - t * h[e];
+              dsp = ds + t * h[e];
+              h[e] = T(0);
+              rot_flag[nflag] = 1;
+            }
+            rc[nb][ns] = c;
+            rs[nb][ns] = s;
+            rt[nb][ns] = t;
+            rdp[nb][ns] = dfp;
+            rdq[nb][ns] = dsp;
+          }
+          G[idx[e]] = h[e];
+        }
       }
-      // (3) Q <- Q J in registers (fp64): (c, s) from t, normalised in fp64
+      EVD_T(1);
+      // Q <- Q J in registers (fp64): (c, s) of step st from t, normalised in fp64
       {
-        const T tq = prm_t[slot];
+        const T tq = rt[b][slot];
         if (tq != T(0)) {
           double c64, s64;
           if constexpr (sizeof(T) == 8) {
-            c64 = prm_cs[slot].c;
-            s64 = prm_cs[slot].s;
+            c64 = rc[b][slot];
+            s64 = rs[b][slot];
           } else {
             const double td = (double)tq;
             c64 = rsqrt64(1.0 + td * td);
@@ -482,10 +525,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
           }
         }
       }
-      EVD_T(3);
-      __syncthreads();
-      EVD_T(4);
-      // (4) advance the round robin: firsts shift right, seconds shift left
+      // advance the round robin: firsts shift right, seconds shift left
 #pragma unroll
       for (int i = 0; i < RPL; ++i) {
         const double f_r = dpp_shr1(qf[i]), s_r = dpp_shr1(qs[i]), s_l = dpp_shl1(qs[i]);
@@ -501,19 +541,15 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         pf = nf;
         ps = ns;
       }
-      EVD_T(5);
+      EVD_T(2);
+      __syncthreads();
+      EVD_T(3);
       EVD_ACC(0, 0, 1);
       EVD_ACC(1, 1, 2);
       EVD_ACC(2, 2, 3);
-      EVD_ACC(3, 3, 4);
-      EVD_ACC(4, 4, 5);
     }
-    const int rot = sweep_rot;
-    __syncthreads();
-    if (tid == 0) sweep_rot = 0;
-    if (!rot) break;
+    if (!rot_flag[sw & 1]) break;
     any = true;
-    __syncthreads();
   }
 
   if (tid == 0) {
@@ -530,16 +566,19 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       qo[k * N + pf] = (T)qf[i];
       qo[k * N + ps] = (T)qs[i];
     }
-  }
-  for (int a = tid; a < N; a += NT) {
-    const int col = (a < W ? bi * W + a : bj * W + (a - W));
-    D[col] = G[a * LD + a];
+    // diagonals after the last executed step (records of step gs - 1)
+    if (tid < W) {
+      const int lb = (gs - 1) & 1;
+      int p, q;
+      ring_slot<W>(tid, R - 1, p, q);
+      D[p < W ? bi * W + p : bj * W + (p - W)] = rdp[lb][tid];
+      D[q < W ? bi * W + q : bj * W + (q - W)] = rdq[lb][tid];
+    }
+  } else {
+    for (int a = tid; a < N; a += NT)
+      D[a < W ? bi * W + a : bj * W + (a - W)] = G[a * LD + a];
   }
 }
-
-}  // namespace svdj
-#include "evd2.hpp"
-namespace svdj {
 
 // ------------------------------------------------------------------ apply
 #ifndef SVDJ_APPLY_QPD
@@ -852,7 +891,7 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
-  // slabs + double-buffered Q and skip flags (V update runs one step behind)
+  // slabs + double-buffered Q and skip flags (evd(s+1) may run while apply(s) reads)
   return ((slabs + 255) / 256 * 256) + 2 * ((q + 255) / 256 * 256) + 2 * ((sk + 255) / 256 * 256);
 }
 
@@ -913,13 +952,6 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int max_inner, 
     hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
                        c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   SVDJ_LAUNCH_CHECK();
-#if defined(SVDJ_EVD2)
-  // Two-level EVD (evd2.hpp): measured slower on MI355X, kept opt-in.
-  if constexpr (W == 32)
-    hipLaunchKernelGGL((evd2_kernel<T>), dim3(c.P), dim3(kEvd2Threads), 0, c.st, pr, full,
-                       c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, max_inner, metric);
-  else
-#endif
     hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
                        c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, max_inner, metric);
   SVDJ_LAUNCH_CHECK();
@@ -973,22 +1005,40 @@ static int block_steps_t(const Chain<T>& c, double tol, int max_inner, uint32_t*
   return 0;
 }
 
-// Recycled cross-stream events of the staggered two-chain issue (one ring per
-// device; a wait captures the event's state when it is enqueued, so an event
-// can be re-recorded once its waits are issued).
-static hipEvent_t* stagger_events(int& n) {
-  constexpr int kMaxDev = 64, kRing = 64;
-  static hipEvent_t ev[kMaxDev][kRing];
-  static bool made[kMaxDev] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-  if (!made[dev]) {
-    for (int i = 0; i < kRing; ++i)
-      if (hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess) return nullptr;
-    made[dev] = true;
-  }
+// Recycled cross-stream events of the staggered two-chain issue.  One ring per
+// (recording stream, waiting stream) pair, created on the device the streams
+// belong to (not the caller's current device) and looked up under a mutex, so
+// solvers on several devices or host threads never share an event.  A wait
+// captures the event's state when it is enqueued, so an event can be
+// re-recorded once its waits are issued -- within ONE stream pair, whose
+// issue order the caller serialises.
+static hipEvent_t* stagger_events(hipStream_t rec, hipStream_t wait, int& n) {
+  constexpr int kRing = 64;
+  struct Ring {
+    hipStream_t rec, wait;
+    hipEvent_t ev[kRing];
+  };
+  static std::mutex mu;
+  static std::vector<Ring*> rings;
+  std::lock_guard<std::mutex> lock(mu);
   n = kRing;
-  return ev[dev];
+  for (Ring* r : rings)
+    if (r->rec == rec && r->wait == wait) return r->ev;
+  int sdev = 0, cur = 0;
+  if (hipStreamGetDevice(rec, &sdev) != hipSuccess || hipGetDevice(&cur) != hipSuccess)
+    return nullptr;
+  if (sdev != cur && hipSetDevice(sdev) != hipSuccess) return nullptr;
+  Ring* r = new Ring{rec, wait, {}};
+  bool ok = true;
+  for (int i = 0; i < kRing && ok; ++i)
+    ok = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming) == hipSuccess;
+  if (sdev != cur) (void)hipSetDevice(cur);
+  if (!ok) {
+    delete r;  // (events created before the failure are leaked; error path only)
+    return nullptr;
+  }
+  rings.push_back(r);
+  return r->ev;
 }
 
 // Two independent chains on two streams, staggered: chain B's step s starts
@@ -1002,7 +1052,7 @@ template <typename T, int W>
 static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int max_inner,
                           uint32_t* metric, int mma) {
   int ne = 0;
-  hipEvent_t* ev = stagger_events(ne);
+  hipEvent_t* ev = stagger_events(a.st, b.st, ne);
   if (!ev) {
     set_error("stagger events unavailable");
     return -100;

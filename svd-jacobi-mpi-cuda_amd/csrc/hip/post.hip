@@ -70,9 +70,31 @@ __global__ __launch_bounds__(256) void finalize_kernel(T* __restrict__ A, int m_
   }
 }
 
+// One-lane timed wait on a stream (the simulated-exchange link model of
+// parallel/comm.py SimCommunicator): returns once the constant-rate wall
+// clock has advanced by `ticks` (always terminates; sleeps between polls).
+__global__ __launch_bounds__(64) void spin_kernel(unsigned long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 }  // namespace svdj
 
 using namespace svdj;
+
+extern "C" int svdj_spin_ns(double ns, void* stream) {
+  if (!(ns > 0.0)) return 0;
+  const double cap = 10e9;  // 10 s: a modelled transfer never needs more
+  int dev = 0, khz = 0;
+  SVDJ_HIP_CHECK(hipStreamGetDevice((hipStream_t)stream, &dev));
+  SVDJ_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;  // 100 MHz on gfx9
+  const unsigned long long ticks = (unsigned long long)((ns < cap ? ns : cap) * 1e-6 * khz);
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" const char* svdj_hip_last_error(void) { return g_err; }
 

@@ -106,6 +106,10 @@ int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int ncols, voi
 // sigma[c] = ||a_c||; if scale_u, a_c /= sigma[c] (sigma == 0 columns untouched).
 int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma, int scale_u, void* stream);
 
+// Device-side timed wait of `ns` nanoseconds on `stream` (one lane polling
+// the constant 100 MHz clock); used to model link time in simulations.
+int svdj_spin_ns(double ns, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

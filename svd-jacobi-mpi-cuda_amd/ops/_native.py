@@ -124,6 +124,7 @@ def hip_lib():
         _sig(lib, "svdj_col_norms2", c_int, [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_finalize", c_int,
              [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p])
+        _sig(lib, "svdj_spin_ns", c_int, [c_double, c_void_p])
         _hip = lib
         return lib
 

@@ -132,6 +132,13 @@ def finalize(At: torch.Tensor, m_pad: int, scale_u: bool = True) -> torch.Tensor
     return sigma
 
 
+def spin_ns(device, ns: float):
+    """Enqueue a device-side wait of ``ns`` nanoseconds on the current stream
+    of ``device`` (link-time model of the simulated exchange)."""
+    st = C.c_void_p(torch.cuda.current_stream(torch.device(device)).cuda_stream)
+    hip_check(hip_lib().svdj_spin_ns(float(ns), st), "spin_ns")
+
+
 # ---------------------------------------------------------------- scalar path
 def scalar_step(At, Vt, m_pad, pairs, tol, tol_mode, metric):
     """One parallel step; pairs: int32 tensor (k, 2) on At's device."""
@@ -180,14 +187,19 @@ def scalar_solve(At, Vt, m_pad, sched, tol, tol_mode, max_sweeps):
 _WS_CACHE: dict = {}
 
 
-def block_workspace(dtype, W, P, m_pad, device, slot: int = 0) -> torch.Tensor:
-    """Per (device, shape, slot) workspace; concurrent chains use distinct slots."""
+def block_workspace(dtype, W, P, m_pad, device, slot: int = 0, pool: dict | None = None
+                    ) -> torch.Tensor:
+    """Per (device, shape, slot) workspace; concurrent chains use distinct
+    slots.  ``pool`` is the caller's own cache (a solver instance owns one, so
+    solvers running concurrently -- e.g. several ranks in one process -- never
+    share scratch); None uses the module-wide cache."""
     nbytes = int(hip_lib().svdj_block_workspace_bytes(dtype_code(dtype), W, P, m_pad))
+    cache = _WS_CACHE if pool is None else pool
     key = (torch.device(device), dtype, W, P, m_pad, slot)
-    ws = _WS_CACHE.get(key)
+    ws = cache.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        _WS_CACHE[key] = ws
+        cache[key] = ws
     return ws
 
 
@@ -198,7 +210,7 @@ def check_block(dtype, W):
 
 
 def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0,
-                mma="native"):
+                mma="native", pool: dict | None = None):
     """Run ``len(modes)`` block steps on the current stream.  pairs: int32
     (steps, P, 2) on At's device (block indices local to At); modes: list of
     0 (cross) / 1 (full).  Chains running concurrently on different streams
@@ -209,7 +221,7 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
     if steps == 0 or P == 0:
         return
     if At.is_cuda:
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, ws_slot)
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, ws_slot, pool)
         md = (C.c_int32 * steps)(*[int(x) for x in modes])
         n_v = Vt.shape[1] if Vt is not None else 0
         ldv = Vt.stride(0) if Vt is not None else 0
@@ -225,7 +237,8 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             metric[1] += nrot
 
 
-def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native"):
+def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native",
+                 pool: dict | None = None):
     """Two independent chains of block steps, staggered (svdj_block_steps2).
     ``chain_x = (pairs, modes, ws_slot, stream)``: device pairs (steps, P, 2),
     host modes, a workspace slot and the torch stream of that chain.  Step s
@@ -233,14 +246,14 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     the chains run one after the other."""
     if not At.is_cuda:
         for pairs, modes, slot, _ in (chain_a, chain_b):
-            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma)
+            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool)
         return
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
     args = []
     for pairs, modes, slot, stream in (chain_a, chain_b):
         steps, P = int(pairs.shape[0]), int(pairs.shape[1])
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot)
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool)
         md = (C.c_int32 * max(steps, 1))(*[int(x) for x in modes])
         args.append((_ptr(pairs), P, steps, md, _ptr(ws), ws.numel(),
                      C.c_void_p(stream.cuda_stream)))

@@ -11,6 +11,21 @@ SURVEY.md section 2.4) with torch.distributed:
 Every rank calls the same sequence; there is no root in the hot loop.  The
 convergence value is an all-reduce (max of the off value, sum of rotations),
 which the reference computed and dropped (main.cu:710).
+
+Two single-GPU rehearsal modes exist besides the production path:
+
+* ``SVDJ_SHARED_GPU=1`` with the nccl backend: P processes share cuda:0 and
+  still talk through RCCL.  RCCL refuses two ranks on one device of one host
+  ("Duplicate GPU detected"), so each rank declares its own host identity
+  (``NCCL_HOSTID``) and the ranks connect through RCCL's socket transport on
+  the loopback interface.  The transport is not xGMI, but the torch/RCCL
+  stream and event semantics the pipelined exchange relies on are the real
+  ones, with no host synchronisation anywhere in the sweep.
+* :class:`SimCommunicator`: ONE process plays rank g of a P-rank job; each
+  exchange swaps the outgoing half super-block with one held by a simulated
+  peer (device copies of exactly the real message sizes, optionally padded to
+  the modelled xGMI link time).  It measures the true per-GPU compute time of
+  rank g's sweep plan at P = 2, 4, 8 on one GPU.
 """
 from __future__ import annotations
 
@@ -26,31 +41,47 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def default_timeout_s() -> float:
+    """Process-group timeout: ``SVDJ_COMM_TIMEOUT`` seconds (default 600).  A
+    collective or p2p op that does not finish in time makes the RCCL watchdog
+    abort the process (TORCH_NCCL_ASYNC_ERROR_HANDLING), so a hung peer ends
+    the job with a non-zero exit instead of hanging it."""
+    return float(os.environ.get("SVDJ_COMM_TIMEOUT", "600"))
+
+
 class Communicator:
     """Thin wrapper over a torch.distributed process group."""
 
     def __init__(self, backend: str | None = None, device: torch.device | None = None,
-                 timeout_s: float = 600.0, init: bool = True):
+                 timeout_s: float | None = None, init: bool = True):
         rank, world, local = env_world()
+        shared = os.environ.get("SVDJ_SHARED_GPU") == "1"
         if device is None:
             # SVDJ_SHARED_GPU=1: every rank on cuda:0 (rehearsing the multi-rank
-            # RCCL path on a one-GPU box; not a performance configuration)
-            idx = 0 if os.environ.get("SVDJ_SHARED_GPU") == "1" else local
+            # path on a one-GPU box; not a performance configuration)
+            idx = 0 if shared else local
             device = torch.device("cuda", idx) if torch.cuda.is_available() else torch.device("cpu")
         self.device = torch.device(device)
         if backend is None:
             backend = os.environ.get("SVDJ_COMM_BACKEND") or (
                 "nccl" if self.device.type == "cuda" else "gloo")
         self.backend = backend
+        self.timeout_s = default_timeout_s() if timeout_s is None else float(timeout_s)
         self.owns_group = False
         if world > 1 and init and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            # fail fast: a timed-out RCCL op aborts the process
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            if backend == "nccl" and shared:
+                os.environ["NCCL_HOSTID"] = f"svdj-shared-gpu-rank{rank}"
+                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+                os.environ.setdefault("NCCL_IB_DISABLE", "1")
             kw = {}
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
                 kw["device_id"] = self.device
-            dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s),
-                                    **kw)
+            dist.init_process_group(backend=backend,
+                                    timeout=datetime.timedelta(seconds=self.timeout_s), **kw)
             self.owns_group = True
         self.rank = dist.get_rank() if dist.is_initialized() else rank
         self.world = dist.get_world_size() if dist.is_initialized() else world
@@ -59,13 +90,24 @@ class Communicator:
     def distributed(self) -> bool:
         return self.world > 1
 
+    @property
+    def async_device(self) -> bool:
+        """True when p2p on device tensors is stream-ordered (RCCL): the
+        exchange is enqueued after the issuing stream's work and completion is
+        a stream dependency, never a host wait."""
+        return self.backend == "nccl" and self.device.type == "cuda"
+
     # ---------------------------------------------------------------- p2p
+    def _ops(self, sends: list, recvs: list) -> list:
+        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends if d != self.rank]
+        ops += [dist.P2POp(dist.irecv, t, s) for t, s in recvs if s != self.rank]
+        return ops
+
     def sendrecv(self, sends: list, recvs: list):
         """Grouped point-to-point: sends = [(tensor, dst)], recvs = [(tensor, src)]."""
         if not self.distributed:
             raise RuntimeError("sendrecv on a single rank")
-        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends if d != self.rank]
-        ops += [dist.P2POp(dist.irecv, t, s) for t, s in recvs if s != self.rank]
+        ops = self._ops(sends, recvs)
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
@@ -77,8 +119,7 @@ class Communicator:
         the host) depend on it -- so compute on other streams overlaps it."""
         if not self.distributed:
             raise RuntimeError("isendrecv on a single rank")
-        ops = [dist.P2POp(dist.isend, t, d) for t, d in sends if d != self.rank]
-        ops += [dist.P2POp(dist.irecv, t, s) for t, s in recvs if s != self.rank]
+        ops = self._ops(sends, recvs)
         return dist.batch_isend_irecv(ops) if ops else []
 
     # ---------------------------------------------------------- collectives
@@ -94,6 +135,12 @@ class Communicator:
             t = torch.cat([a, b])
         h = t.cpu()
         return float(h[0]), float(h[1])
+
+    def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks (device tensors: RCCL, stream-ordered)."""
+        if self.distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
 
     def barrier(self):
         if self.distributed:
@@ -118,3 +165,101 @@ class Communicator:
         if self.owns_group and dist.is_initialized():
             dist.destroy_process_group()
             self.owns_group = False
+
+
+class _StreamWork:
+    """Completion handle of a simulated exchange: ``wait()`` makes the
+    CURRENT stream wait for it (the RCCL work semantics)."""
+
+    def __init__(self, event: torch.cuda.Event | None):
+        self.event = event
+
+    def wait(self):
+        if self.event is not None:
+            torch.cuda.current_stream().wait_event(self.event)
+
+
+class SimCommunicator:
+    """Rank ``rank`` of a simulated ``world``-rank job, in one process.
+
+    Collectives are local (the simulated peers are taken to agree), and
+    every exchange is a swap with a simulated peer: the received tensor is
+    one the simulated ring sent earlier (initially ``seed_fn(pos, like)`` for
+    message slot ``pos`` -- other columns of the same matrix), and the sent
+    tensor joins the ring.  The ring holds ``2*world - 2`` entries per message shape, like the
+    super-blocks held by the other ranks, so a received half was never paired
+    with this rank's blocks in the current round and the EVDs keep real
+    rotation work.  The numerics are therefore NOT those of the real job
+    (sweep counts do not converge like it); use this for per-sweep time.
+
+    ``link_gbps`` > 0 pads every exchange on the comm stream with a device
+    spin of the modelled transfer time (bytes of the larger direction over
+    the link bandwidth), so the overlap with compute can be studied.
+    """
+
+    backend = "sim"
+
+    def __init__(self, world: int, rank: int, device: torch.device, seed_fn=None,
+                 link_gbps: float = 0.0):
+        if not (0 <= rank < world):
+            raise ValueError(f"rank {rank} not in world {world}")
+        self.world, self.rank = int(world), int(rank)
+        self.device = torch.device(device)
+        self.timeout_s = 0.0
+        self.owns_group = False
+        self.seed_fn = seed_fn
+        self.link_gbps = float(link_gbps)
+        self._ring: dict = {}
+        self.bytes_moved = 0
+        self.exchanges = 0
+
+    distributed = property(lambda self: self.world > 1)
+    async_device = property(lambda self: self.device.type == "cuda")
+
+    def _swap(self, sends: list, recvs: list):
+        nbytes = 0
+        for pos, ((st, _), (rt, _)) in enumerate(zip(sends, recvs)):
+            key = (pos, tuple(rt.shape), rt.dtype)  # one ring per message slot
+            ring = self._ring.setdefault(key, [])
+            depth = max(2 * self.world - 2, 1)
+            while len(ring) < depth:
+                ring.append(self.seed_fn(pos, rt) if self.seed_fn else torch.zeros_like(rt))
+            src = ring.pop(0)
+            rt.copy_(src)
+            src.copy_(st)  # reuse the storage for the outgoing tensor
+            ring.append(src)
+            nbytes += st.numel() * st.element_size()
+        self.bytes_moved += nbytes
+        self.exchanges += 1
+        if self.link_gbps > 0 and self.device.type == "cuda":
+            from ..ops import kernels as K
+            K.spin_ns(self.device, nbytes / (self.link_gbps * 1e9) * 1e9)
+
+    def sendrecv(self, sends: list, recvs: list):
+        self._swap(sends, recvs)
+
+    def isendrecv(self, sends: list, recvs: list) -> list:
+        self._swap(sends, recvs)
+        if self.device.type != "cuda":
+            return []
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return [_StreamWork(ev)]
+
+    def allreduce_max_sum(self, mx, cnt):
+        return float(torch.as_tensor(mx).double()), float(torch.as_tensor(cnt).double())
+
+    def allreduce_sum_(self, t):
+        return t
+
+    def barrier(self):
+        pass
+
+    def broadcast(self, t, src: int = 0):
+        return t
+
+    def max_over_ranks(self, x: float) -> float:
+        return float(x)
+
+    def destroy(self):
+        pass

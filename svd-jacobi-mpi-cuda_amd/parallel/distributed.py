@@ -51,6 +51,7 @@ class DistributedBlockJacobi(Solver):
     def __init__(self, config: SolverConfig | None = None, comm: Communicator | None = None):
         super().__init__(config)
         self.comm = comm or Communicator()
+        self._ws = {}  # this solver's kernel workspaces (never shared with another solver)
 
     # ------------------------------------------------------------ geometry
     def geometry(self, m: int, n: int, dtype: torch.dtype):
@@ -191,15 +192,15 @@ class DistributedBlockJacobi(Solver):
         converged = False
         bufs = (rA, rV, rD)
         if pipelined:
-            ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour)
+            ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing)
 
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
-                              metric, slot, mma=mma)
+                              metric, slot, mma=mma, pool=self._ws)
 
             def run_pair(a, b):
                 K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
-                               mma=mma)
+                               mma=mma, pool=self._ws)
 
             if not cfg.stagger:
                 run_pair = None
@@ -218,12 +219,12 @@ class DistributedBlockJacobi(Solver):
                         t_comm += time.perf_counter() - tc
                     with trace_range(f"svdj.round{r}"):
                         K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                      cfg.max_inner_sweeps, metric, mma=mma)
+                                      cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
             if cfg.progress and g == 0:
-                print(f"[svdj] sweep {sweeps}: off {mx:.3e}, rotated pairs {nrot}, "
+                print(f"[svdj] sweep {sweeps}: off {mx:.3e}, rotated pairs {int(nrot)}, "
                       f"{time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
             if nrot == 0:
                 converged = True
@@ -242,6 +243,8 @@ class DistributedBlockJacobi(Solver):
         t_total = time.perf_counter() - t0
         info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
+        if pipelined and P > 1:
+            info["comm"] = ex.comm_summary()
         if time_only or not gather:
             return SVDResult(At if jobu != SVDOptions.NoVec else None, sigma_loc, Vt, sweeps, hist,
                              t_total, self.name, {**info, "distributed_output": True})
@@ -279,7 +282,8 @@ class DistributedBlockJacobi(Solver):
         if Vt is not None:
             sends.append((Vt[sl], dst))
             recvs.append((rV, src))
-        host_sync = At.is_cuda and self.comm.backend != "nccl"  # gloo rehearsal, see pipeline.py
+        # gloo on device tensors (rehearsal) is not stream-ordered, see pipeline.py
+        host_sync = At.is_cuda and not getattr(self.comm, "async_device", False)
         if host_sync:
             torch.cuda.synchronize(At.device)
         self.comm.sendrecv(sends, recvs)
@@ -318,9 +322,14 @@ class DistributedBlockJacobi(Solver):
                 if c1 > c0:
                     At[s * B:s * B + (c1 - c0), :m].copy_(A[:, c0:c1].t())
             return
+        # Root-owned input: rank 0 packs every rank's two super-blocks and
+        # posts all P-1 sends as ONE grouped batch, so the transfers run
+        # concurrently over the P-1 xGMI links (the reference's scatter is a
+        # serial loop of blocking sends, main.cu:582-619).
         tour = tournament(comm.world)
         if comm.rank == 0:
             Ad = A.to(device=At.device, dtype=At.dtype)
+            sends = []
             for dst in range(comm.world):
                 buf = torch.zeros_like(At) if dst != 0 else At
                 for s in range(2):
@@ -329,7 +338,8 @@ class DistributedBlockJacobi(Solver):
                     if c1 > c0:
                         buf[s * B:s * B + (c1 - c0), :m].copy_(Ad[:, c0:c1].t())
                 if dst != 0:
-                    comm.sendrecv([(buf, dst)], [])
+                    sends.append((buf, dst))
+            comm.sendrecv(sends, [])
         else:
             comm.sendrecv([], [(At, 0)])
 
@@ -357,14 +367,17 @@ class DistributedBlockJacobi(Solver):
         if not comm.distributed:
             parts = [(ids, At, Vt, sigma)]
         elif comm.rank == 0:
+            # all P-1 ranks' blocks arrive in one grouped batch (concurrent
+            # links; the reference gathers rank by rank, main.cu:854-936)
             parts = [(ids, At, Vt, sigma)]
+            recvs = []
             for src in range(1, comm.world):
                 rid = torch.empty_like(ids)
                 rA, rS = torch.empty_like(At), torch.empty_like(sigma)
                 rV = torch.empty_like(Vt) if want_v else None
-                recvs = [(rid, src), (rA, src), (rS, src)] + ([(rV, src)] if want_v else [])
-                comm.sendrecv([], recvs)
+                recvs += [(rid, src), (rA, src), (rS, src)] + ([(rV, src)] if want_v else [])
                 parts.append((rid, rA, rV, rS))
+            comm.sendrecv([], recvs)
         else:
             sends = [(ids, 0), (At, 0), (sigma, 0)] + ([(Vt, 0)] if want_v else [])
             comm.sendrecv(sends, [])

@@ -192,9 +192,19 @@ def _global_block(place_g, b: int, k: int, h: int) -> int:
 
 
 class PipelineExecutor:
-    """Runs a :class:`SweepPlan` on the resident buffers of one rank."""
+    """Runs a :class:`SweepPlan` on the resident buffers of one rank.
 
-    def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour):
+    Exchange timing (``timing=True``, device runs with a stream-ordered
+    communicator): every half exchange is bracketed on the comm stream by two
+    timing events (issue after its producers' events, arrival of both
+    directions), and every consumer records an event on its own stream just
+    before it starts waiting for the arrival.  :meth:`comm_summary` turns them
+    into ``comm_ms`` (sum of exchange spans, including waiting for the peer)
+    and ``exposed_comm_ms`` (sum over consumers of how long the arrival
+    trailed the moment the consumer stream was ready -- the part of the
+    exchange not hidden under compute)."""
+
+    def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour, timing: bool = False):
         self.comm, self.streams = comm, streams
         self.At, self.Vt, self.D = At, Vt, D
         self.k, self.W, self.tour = k, W, tour
@@ -209,6 +219,12 @@ class PipelineExecutor:
         self.dev_pairs = {}  # item index -> device pairs (the plan is fixed per solve)
         self._groups = {}
         self.comm_stream = torch.cuda.Stream(dev) if self.cuda and comm.distributed else None
+        self.stream_ordered = self.cuda and getattr(comm, "async_device", False)
+        self.timing = bool(timing) and self.stream_ordered
+        self._t0 = None
+        self._spans = []     # (issue event, arrival event) per half exchange
+        self._waits = []     # (consumer-ready event, arrival event) per consume
+        self.bytes_sent = 0
 
     def _rows(self, slot: int, half: int) -> slice:
         b0 = slot * self.k * self.W + half * self.hB
@@ -234,6 +250,9 @@ class PipelineExecutor:
             # reset, initial norms) happens before any task or exchange
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(self.At.device))
+            if self.timing and self._t0 is None:
+                self._t0 = torch.cuda.Event(enable_timing=True)
+                self._t0.record(torch.cuda.current_stream(self.At.device))
             for s in self.streams + ([self.comm_stream] if self.comm_stream else []):
                 s.wait_event(ready)
         last = {}       # (slot, half) -> [events of tasks since last exchange]
@@ -299,6 +318,7 @@ class PipelineExecutor:
         if self.Vt is not None:
             sends.append((self.Vt[sl], dst))
             recvs.append((rV, src))
+        self.bytes_sent += sum(t.numel() * t.element_size() for t, _ in sends)
         if not comm.distributed:
             raise RuntimeError("exchange on a single rank")
         if not self.cuda:
@@ -309,24 +329,61 @@ class PipelineExecutor:
         cs = self.comm_stream
         for ev in last.pop((x, hh), ()):
             cs.wait_event(ev)
-        if comm.backend != "nccl":
+        if not self.stream_ordered:
             # gloo on device tensors (one-GPU rehearsal of the multi-rank
             # path) does not order its copies after other streams: make the
             # data ready on the host side first.  RCCL needs none of this.
             cs.synchronize()
+            with torch.cuda.stream(cs):
+                pending[(x, hh)] = comm.isendrecv(sends, recvs)
+            return
+        # Stream-ordered (RCCL): the comm stream issues the grouped send/recv
+        # after the producers' events, then waits (device-side) for both
+        # directions; consumers wait on ONE arrival event -- no host sync.
         with torch.cuda.stream(cs):
-            works = comm.isendrecv(sends, recvs)
-        pending[(x, hh)] = works
+            t_issue = None
+            if self.timing:
+                t_issue = torch.cuda.Event(enable_timing=True)
+                t_issue.record(cs)
+            for w in comm.isendrecv(sends, recvs):
+                w.wait()
+            arrived = torch.cuda.Event(enable_timing=self.timing)
+            arrived.record(cs)
+        if self.timing:
+            self._spans.append((t_issue, arrived))
+        pending[(x, hh)] = arrived
 
     def _consume(self, hv, pending):
-        works = pending.pop(hv, None)
-        if works is None:
+        got = pending.pop(hv, None)
+        if got is None:
             return
-        for w in works:
-            w.wait()  # current (consumer) stream waits for send + recv
-        if self.cuda and self.comm.backend != "nccl":
-            torch.cuda.synchronize(self.At.device)
+        if self.stream_ordered:
+            s = torch.cuda.current_stream(self.At.device)
+            if self.timing:
+                ready = torch.cuda.Event(enable_timing=True)
+                ready.record(s)
+                self._waits.append((ready, got))
+            s.wait_event(got)
+        else:
+            for w in got:
+                w.wait()  # gloo: blocks the host until both directions are done
+            if self.cuda:
+                torch.cuda.synchronize(self.At.device)
         self._copy_in(self._rows(*hv), hv[1])
+
+    def comm_summary(self) -> dict:
+        """Exchange timing of every sweep run so far (synchronises)."""
+        out = {"exchanges": len(self._spans), "bytes_sent": int(self.bytes_sent)}
+        if not self.timing or self._t0 is None:
+            return out
+        torch.cuda.synchronize(self.At.device)
+        out["comm_ms"] = round(sum(a.elapsed_time(b) for a, b in self._spans), 3)
+        t0 = self._t0
+        exposed = 0.0
+        for ready, arrived in self._waits:
+            exposed += max(0.0, t0.elapsed_time(arrived) - t0.elapsed_time(ready))
+        out["exposed_comm_ms"] = round(exposed, 3)
+        return out
 
     def _copy_in(self, sl, hh):
         rA, rV, rD = self.rbuf[hh]

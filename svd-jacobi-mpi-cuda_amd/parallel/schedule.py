@@ -134,45 +134,6 @@ class RoundPlan:
     modes: list         # per step 0 cross / 1 full
 
 
-@dataclass
-class Chain:
-    pairs: np.ndarray   # (steps, pairs_per_step, 2) local block indices
-    modes: list
-
-
-def _bip(xs: list, ys: list) -> np.ndarray:
-    h = len(xs)
-    out = np.zeros((h, h, 2), dtype=np.int32)
-    for t in range(h):
-        for a in range(h):
-            out[t, a] = (xs[a], ys[(a + t) % h])
-    return out
-
-
-def chained_sweep_plan(P: int, k: int) -> list:
-    """Like :func:`distributed_sweep_plan` but every round is a list of PHASES,
-    each phase a list of 2 INDEPENDENT chains (disjoint blocks), so the two
-    chains can run on two HIP streams and one chain's latency-bound EVD
-    overlaps the other chain's bandwidth-bound Gram/apply.
-
-    With X = slot 0 blocks [0,k), Y = slot 1 blocks [k,2k), each split in
-    halves X0|X1, Y0|Y1 (k even):
-      round 0 : [RR(X) || RR(Y)], [X0xY0 || X1xY1], [X0xY1 || X1xY0]
-      round r : [X0xY0 || X1xY1], [X0xY1 || X1xY0]
-    Every block pair is still visited exactly once per sweep.  Returns None
-    when k is odd or < 2 (use the single-chain plan)."""
-    if k < 2 or k % 2:
-        return None
-    h = k // 2
-    X0, X1 = list(range(0, h)), list(range(h, k))
-    Y0, Y1 = list(range(k, k + h)), list(range(k + h, 2 * k))
-    rr = round_robin(k)
-    cross = [[Chain(_bip(X0, Y0), [0] * h), Chain(_bip(X1, Y1), [0] * h)],
-             [Chain(_bip(X0, Y1), [0] * h), Chain(_bip(X1, Y0), [0] * h)]]
-    round0 = [[Chain(rr.copy(), [1] + [0] * (k - 2)), Chain(rr + k, [1] + [0] * (k - 2))]] + cross
-    return [round0] + [cross for _ in range(1, 2 * P - 1)]
-
-
 def distributed_sweep_plan(P: int, k: int) -> list:
     """Per-round local plans for a sweep with P GPUs, k blocks per super-block.
 

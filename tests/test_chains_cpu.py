@@ -1,45 +1,10 @@
-"""Chained (two-stream) sweep plans: coverage and CPU equivalence."""
-import pytest
+"""Two-chain (pipelined) solver: CPU equivalence with the single-chain path.
+
+Plan coverage of the pipelined sweep is checked in test_pipeline_cpu.py."""
 import torch
 
 import svdj
 from svdj.parallel import Communicator, DistributedBlockJacobi
-from svdj.parallel import schedule as S
-
-
-@pytest.mark.parametrize("P,k", [(1, 2), (1, 4), (2, 2), (3, 4), (4, 2)])
-def test_chained_plan_covers_every_pair_once(P, k):
-    t = S.tournament(P)
-    plans = S.chained_sweep_plan(P, k)
-    phys = [[int(t.held[0, g, 0]), int(t.held[0, g, 1])] for g in range(P)]
-    seen = set()
-    for r in range(t.rounds):
-        if r > 0:
-            old = [list(x) for x in phys]
-            for g in range(P):
-                src = int(t.recv_from[r, g])
-                phys[g][int(t.xslot[r, g])] = old[src][int(t.xslot[r, src])]
-        for g in range(P):
-            for phase in plans[r]:
-                used = [set(), set()]
-                for c, chain in enumerate(phase):
-                    for st in chain.pairs:
-                        blocks = st.reshape(-1).tolist()
-                        assert len(blocks) == len(set(blocks))
-                        used[c].update(blocks)
-                        for a, b in st:
-                            ga = phys[g][a // k] * k + a % k
-                            gb = phys[g][b // k] * k + b % k
-                            key = (min(ga, gb), max(ga, gb))
-                            assert key not in seen
-                            seen.add(key)
-                assert not (used[0] & used[1]), "chains of a phase must be independent"
-    nb = 2 * P * k
-    assert len(seen) == nb * (nb - 1) // 2
-
-
-def test_chained_plan_odd_k_falls_back():
-    assert S.chained_sweep_plan(2, 3) is None
 
 
 def test_chained_solver_cpu_matches_single_chain():

@@ -1,4 +1,4 @@
-"""Multi-process distributed block Jacobi on CPU (gloo), world 1..4."""
+"""Multi-process distributed block Jacobi on CPU (gloo), world 1..4 and 8."""
 import json
 import os
 import socket
@@ -29,7 +29,8 @@ def _run(world, m, n, W, tmp_path, mode="root"):
     return json.loads(out.read_text())
 
 
-@pytest.mark.parametrize("world,m,n", [(1, 140, 128), (2, 160, 128), (3, 200, 190), (4, 300, 256)])
+@pytest.mark.parametrize("world,m,n", [(1, 140, 128), (2, 160, 128), (3, 200, 190), (4, 300, 256),
+                                        (8, 200, 192)])
 def test_distributed_block_jacobi_gloo(world, m, n, tmp_path):
     rep = _run(world, m, n, 32, tmp_path)
     assert rep["converged"] and rep["world"] == world
@@ -66,3 +67,30 @@ def test_isend_irecv_ring(world, tmp_path):
 def test_svd_on_the_fly_api(tmp_path):
     rep = _run(2, 170, 128, 32, tmp_path, mode="otf")
     assert rep["converged"] and rep["residual_rel"] < 1e-12, rep
+
+
+def test_simulated_rank_plan_cpu():
+    """SimCommunicator: one process runs rank g's plan of a P-rank job; every
+    exchange swaps real-sized halves with simulated peers."""
+    import torch
+
+    import svdj
+    from svdj.parallel import DistributedBlockJacobi, SimCommunicator
+
+    P, g, n = 4, 1, 256
+    A = svdj.utils.inputs.random_dense(n, n, dtype=torch.float64, seed=3)
+
+    def seed(pos, like):
+        return torch.rand(like.shape, dtype=like.dtype) if pos != 1 else torch.ones_like(like)
+
+    comm = SimCommunicator(P, g, torch.device("cpu"), seed_fn=seed)
+    cfg = svdj.SolverConfig(block=32, dtype=torch.float64, max_sweeps=2)
+    res = DistributedBlockJacobi(cfg, comm).solve(None, m=n, n=n, dtype=torch.float64,
+                                                  generator=lambda c0, c1: A[:, c0:c1],
+                                                  gather=False)
+    assert res.sweeps == 2
+    # 2P-2 exchanges per sweep, each split in two halves
+    assert comm.exchanges == 2 * 2 * (2 * P - 2)
+    geo = res.info["geometry"]
+    half = geo["B"] // 2
+    assert comm.bytes_moved == comm.exchanges * half * 8 * (geo["m_pad"] + 1 + geo["n_v"])
