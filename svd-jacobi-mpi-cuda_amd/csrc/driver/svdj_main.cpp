@@ -72,8 +72,9 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
     const size_t wsb = svdj_block_workspace_bytes(dtype, W, ncols / W / 2, m_pad);
     CHECK(hipMalloc(&ws, wsb));
     if (svdj_col_norms2(dtype, dA, m_pad, m_pad, ncols, dD, st) < 0) goto fail;
-    sweeps = svdj_block_solve(dtype, W, m_pad, dA, m_pad, dV, n_v, n_v, dD, ncols, tol, 1,
-                              max_sweeps, ws, wsb, dmetric, hist.data(), mma, st);
+    sweeps = svdj_block_solve(dtype, W, m_pad, dA, m_pad, dV, n_v, n_v, dD, ncols, tol,
+                              /*tol_mode relative*/ 0, 1, max_sweeps, ws, wsb, dmetric,
+                              hist.data(), mma, st);
   } else {
     const int steps = svdj_sameh_num_steps(n);
     std::vector<int32_t> sched((size_t)steps * (n / 2) * 2);

@@ -160,29 +160,27 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
 // The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair, as a
 // cyclic parallel Jacobi (circle-method round robin: W disjoint rotations per
 // step, 2W-1 steps per sweep):
-//   * G lives in LDS (data precision, upper triangle, indexed by player id);
-//     every off-diagonal slot-pair block (a < b) of a step is owned by one
-//     thread for the whole kernel (the blocks are dealt once);
+//   * G lives in LDS in POSITION space (see pos_next below): every
+//     off-diagonal slot-pair block (a < b) of a step is owned by one thread
+//     for the whole kernel and its LDS addresses are static;
 //   * ONE barrier per step.  The rotations of step st+1 are solved inside
-//     step st's update phase: the coupling g_xy of a next-step pair (x, y)
-//     lies in exactly one off-diagonal block of step st (x and y sit in
-//     different slots there), so the thread owning that block computes the
-//     new g_xy, takes the post-step diagonals of x and y from the step-st
-//     rotation records, solves step st+1's rotation right away and publishes
-//     it (c, s, t and the post-rotation diagonals) into the other half of a
-//     double-buffered record array.  The reference solves every 2x2 on the
-//     host between two kernel launches (main.cu:698-725); the previous kernel
-//     here still needed a solve phase and a second barrier per step;
+//     step st's update phase: the coupling of a next-step pair lies in exactly
+//     one off-diagonal block of step st, always the same one, so its owner
+//     computes the new coupling, takes the post-step diagonals from the
+//     step-st rotation records, solves step st+1's rotation right away and
+//     publishes it (c, s, fp64 c/s and the post-rotation diagonals) into the
+//     other half of a double-buffered record array.  The reference solves
+//     every 2x2 on the host between two kernel launches (main.cu:698-725);
 //   * the rotation accumulator Q lives in REGISTERS in fp64, in "slot layout":
 //     lane (slot a, row group g) holds Q[k][first(a)] and Q[k][second(a)] for
 //     its rows k.  The circle-method movement is a one-lane DPP shift per step
 //     (wave_shr:1 / wave_shl:1); fp64 keeps Q orthogonal to ~1e-16 before it
 //     is rounded to the data type, so V stays orthogonal over hundreds of
 //     block steps;
-//   * the diagonal never lives in G after the start: it travels in the
-//     records (a rotation of slot a changes only d_first and d_second).
+//   * the diagonal never lives in G: it travels in the rotation records (a
+//     rotation of slot a changes only d_first and d_second).
 #ifndef SVDJ_EVD_THREADS_32
-#define SVDJ_EVD_THREADS_32 512
+#define SVDJ_EVD_THREADS_32 1024
 #endif
 #ifndef SVDJ_EVD_THREADS_64
 #define SVDJ_EVD_THREADS_64 1024
@@ -191,11 +189,20 @@ __host__ __device__ constexpr int evd_threads(int W) {
   return W == 64 ? SVDJ_EVD_THREADS_64 : SVDJ_EVD_THREADS_32;
 }
 
+// Lane i <- lane i-1 / i+1 across the wave (DPP wave_shr:1 / wave_shl:1).
+// The edge lane receives 0 (bound_ctrl); every caller overwrites the edge
+// slots by select, so no "old" value (and no register copy) is needed.
 __device__ __forceinline__ int dpp_shr1(int v) {
-  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);  // lane i <- lane i-1
+  return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);
 }
 __device__ __forceinline__ int dpp_shl1(int v) {
-  return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);  // lane i <- lane i+1
+  return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);
+}
+__device__ __forceinline__ float dpp_shr1(float v) {
+  return __int_as_float(dpp_shr1(__float_as_int(v)));
+}
+__device__ __forceinline__ float dpp_shl1(float v) {
+  return __int_as_float(dpp_shl1(__float_as_int(v)));
 }
 __device__ __forceinline__ double dpp_shr1(double v) {
   const long long x = __double_as_longlong(v);
@@ -225,31 +232,43 @@ __device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gp
   return nrm > 0.0 && fabs(gpq) > tol * nrm;
 }
 
-// Fast fp32 rotation (raw v_sqrt/v_rcp/v_rsq, ~1 ulp): only steers G; Q is
-// built from the fp64-normalised (c, s) of t.
+// Rotation of one slot, branch-free (the solve sits on the EVD's critical
+// path; the selects avoid exec-mask branches): c = 1, s = t = 0 when the
+// test fails.  fp32: raw v_sqrt/v_rcp/v_rsq (~1 ulp) -- (c, s) only steer G;
+// the fp64 Q is built from t.
 __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, float tol,
                                               int absmode, float& c, float& s, float& t) {
-  if (!needs_rotation(gpp, gqq, gpq, tol, absmode)) return false;
-  const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * gpq);
+  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode);
+  const float g = rot ? gpq : 1.0f;
+  const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * g);
   const float at = fabsf(tau);
-  float tt = at > 1e18f ? 0.5f * __builtin_amdgcn_rcpf(at)
-                        : __builtin_amdgcn_rcpf(at + __builtin_amdgcn_sqrtf(1.0f + tau * tau));
-  t = tau < 0.0f ? -tt : tt;
-  c = __builtin_amdgcn_rsqf(1.0f + t * t);
+  const float t_big = 0.5f * __builtin_amdgcn_rcpf(at);
+  const float t_reg = __builtin_amdgcn_rcpf(at + __builtin_amdgcn_sqrtf(fmaf(tau, tau, 1.0f)));
+  const float tt = at > 1e18f ? t_big : t_reg;
+  t = rot ? (tau < 0.0f ? -tt : tt) : 0.0f;
+  c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.0f));
   s = t * c;
-  return true;
+  return rot;
 }
 __device__ __forceinline__ bool rotation_fast(double gpp, double gqq, double gpq, double tol,
                                               int absmode, double& c, double& s, double& t) {
-  if (!needs_rotation(gpp, gqq, gpq, tol, absmode)) return false;
-  schur_rotation<double>(gpq, gpp, gqq, c, s, t);
-  return true;
+  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode);
+  const double g = rot ? gpq : 1.0;
+  const double tau = (gqq - gpp) / (2.0 * g);
+  const double at = fabs(tau);
+  const double tt = at > 1e150 ? 0.5 / at : 1.0 / (at + sqrt(fma(tau, tau, 1.0)));
+  t = rot ? (tau < 0.0 ? -tt : tt) : 0.0;
+  c = 1.0 / sqrt(fma(t, t, 1.0));
+  s = t * c;
+  return rot;
 }
-// fp64 1/sqrt(x) for x in [1, 2^60]: hardware estimate + 2 Newton steps.
+// fp64 1/sqrt(x) for x in [1, 2^60]: fp32 hardware estimate (~2^-22) and two
+// Newton steps in fp64 (quadratic: 2^-44, then below fp64 rounding).
 __device__ __forceinline__ double rsqrt64(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * (1.5 - 0.5 * x * y * y);
-  y = y * (1.5 - 0.5 * x * y * y);
+  double y = (double)__builtin_amdgcn_rsqf((float)x);
+  const double hx = 0.5 * x;
+  y = y * (1.5 - hx * y * y);
+  y = y * (1.5 - hx * y * y);
   return y;
 }
 
@@ -282,16 +301,122 @@ __device__ __forceinline__ void ring_slot(int a, int st, int& p, int& q) {
   p = a == 0 ? 2 * W - 1 : ring_player<W>(a - 1, st);
   q = ring_player<W>(2 * W - 2 - a, st);
 }
-// Inverse: slot of player x at step st (0 <= st < R), and whether x is the
-// slot's first.  Encoded as 2*slot + first.
+// ---- position space.  The circle method fixes WHERE things happen and moves
+// the players: ring positions 0..R-1 (R = 2W-1) plus the fixed position R of
+// player N-1; slot a >= 1 owns positions (a-1, 2W-2-a), slot 0 owns (R, R-1).
+// Every step each ring player advances one position, so an off-diagonal G
+// entry at positions (P1, P2) moves to (P1+1, P2+1) (mod R; R stays R).
+// Storing G by POSITION pair -- double-buffered, the update phase reads step
+// st's buffer at the block's positions and writes the moved entries into the
+// other buffer -- makes every thread's LDS addresses static for the whole
+// kernel: no per-step index arithmetic.  Which entries of a block hold the
+// next step's pairs is static as well (next_meeting).
 template <int W>
-__device__ __forceinline__ int ring_where(int x, int st) {
-  constexpr int R = 2 * W - 1;
-  if (x == 2 * W - 1) return 1;  // slot 0, first
-  int pos = (x == 0 ? R - 1 : x - 1) + st;
-  pos -= pos >= R ? R : 0;
-  return pos <= W - 2 ? 2 * (pos + 1) + 1 : 2 * (2 * W - 2 - pos);
+__host__ __device__ constexpr int pos_next(int P) {
+  return P == 2 * W - 1 ? P : (P + 1 == 2 * W - 1 ? 0 : P + 1);
 }
+template <int W>
+__host__ __device__ constexpr int ring_slot_of(int pos) {  // slot of a ring position
+  return pos == 2 * W - 1 ? 0 : (pos <= W - 2 ? pos + 1 : 2 * W - 2 - pos);
+}
+// Where the players now at positions (P1, P2) meet at the NEXT step: returns
+// 2*slot + (the player at P1 is that slot's first), or -1 if they do not.
+template <int W>
+__host__ __device__ constexpr int next_meeting(int P1, int P2) {
+  constexpr int R = 2 * W - 1;
+  if (P1 == R || P2 == R) {
+    const int o = P1 == R ? P2 : P1;
+    if (pos_next<W>(o) != R - 1) return -1;  // N-1 meets the second of slot 0
+    return P1 == R ? 1 : 0;
+  }
+  const int n1 = pos_next<W>(P1), n2 = pos_next<W>(P2);
+  if (ring_slot_of<W>(n1) != ring_slot_of<W>(n2)) return -1;
+  return 2 * ring_slot_of<W>(n1) + (n1 <= W - 2 ? 1 : 0);
+}
+// Packed strict upper triangle of an N x N position-pair matrix.
+template <int N>
+__host__ __device__ constexpr int tri_idx(int i, int j) {
+  const int a = i < j ? i : j, b = i < j ? j : i;
+  return a * N - a * (a + 1) / 2 + (b - a - 1);
+}
+// Position of player x at step 0 (inverse of ring_slot at st = 0).
+template <int W>
+__host__ __device__ constexpr int pos0(int x) {
+  return x == 2 * W - 1 ? 2 * W - 1 : (x == 0 ? 2 * W - 2 : x - 1);
+}
+template <int W>
+__host__ __device__ constexpr int slot_first_pos(int a) { return a == 0 ? 2 * W - 1 : a - 1; }
+template <int W>
+__host__ __device__ constexpr int slot_second_pos(int a) { return 2 * W - 2 - a; }
+template <int W>
+__host__ __device__ constexpr int block_duty(int a, int b) {  // 256*e + meeting, or -1
+  for (int e = 0; e < 4; ++e) {
+    const int x = (e >> 1) ? slot_second_pos<W>(a) : slot_first_pos<W>(a);
+    const int y = (e & 1) ? slot_second_pos<W>(b) : slot_first_pos<W>(b);
+    const int mt = next_meeting<W>(x, y);
+    if (mt >= 0) return 256 * e + mt;
+  }
+  return -1;
+}
+
+// Which slot-pair blocks (a < b) each thread owns, computed at compile time.
+// Thread roles: the W blocks holding the next step's pairs ("duty" blocks:
+// their owners solve the rotations, W = 32 / 64 of them) go to the first W
+// lanes of wave 0 -- the only lanes that solve, so only wave 0 carries the
+// solve latency and it does no Q work; the other blocks follow in rows taken
+// in complementary pairs 0, W-2, 1, W-3, ... (two paired rows hold W blocks,
+// so a wave's lanes share few slots and the record reads broadcast).
+// blk[j * NT + t] = (a << 8) | b of thread t's j-th block, 0xffff if none.
+template <int W, int NT>
+struct EvdDeal {
+  static constexpr int NOFF = W * (W - 1) / 2;
+  static constexpr int MAXOFF = (NOFF + NT - 1) / NT;
+  unsigned short blk[MAXOFF * NT];
+  constexpr EvdDeal() : blk{} {
+    int g = 0;
+    // duty block of each next-step slot s: the positions that slot's players
+    // occupy NOW are one behind its own positions
+    for (int s = 0; s < W; ++s) {
+      const int f = slot_first_pos<W>(s), q = slot_second_pos<W>(s);
+      const int pf = f == 2 * W - 1 ? f : (f == 0 ? 2 * W - 2 : f - 1);
+      const int pq = q == 0 ? 2 * W - 2 : q - 1;
+      int a = ring_slot_of<W>(pf), b = ring_slot_of<W>(pq);
+      if (a > b) {
+        const int x = a;
+        a = b;
+        b = x;
+      }
+      blk[g++] = (unsigned short)((a << 8) | b);
+    }
+    for (int i = 0; i < W - 1; ++i) {
+      const int a = (i & 1) ? W - 2 - (i >> 1) : (i >> 1);
+      for (int b = a + 1; b < W; ++b)
+        if (block_duty<W>(a, b) < 0) blk[g++] = (unsigned short)((a << 8) | b);
+    }
+    for (; g < MAXOFF * NT; ++g) blk[g] = 0xffff;
+  }
+};
+
+// Compile-time check of the dealing: the first W entries are the duty blocks
+// of next-step slots 0..W-1, and every block is dealt exactly once.
+template <int W, int NT>
+constexpr bool evd_deal_ok() {
+  constexpr EvdDeal<W, NT> d{};
+  int seen[W * W] = {};
+  int dealt = 0;
+  for (int g = 0; g < EvdDeal<W, NT>::MAXOFF * NT; ++g) {
+    if (d.blk[g] == 0xffff) continue;
+    const int a = d.blk[g] >> 8, b = d.blk[g] & 255;
+    if (!(a < b && b < W) || seen[a * W + b]++) return false;
+    ++dealt;
+    const int duty = block_duty<W>(a, b);
+    if (g < W && (duty < 0 || ((duty & 255) >> 1) != g)) return false;
+    if (g >= W && duty >= 0) return false;
+  }
+  return dealt == EvdDeal<W, NT>::NOFF;
+}
+static_assert(evd_deal_ok<32, evd_threads(32)>() && evd_deal_ok<64, evd_threads(64)>(),
+              "EVD block dealing");
 
 template <typename T, int W>
 __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
@@ -302,72 +427,112 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   constexpr int NWAVE = NT / SVDJ_WAVE;
   constexpr int N = 2 * W;
   constexpr int R = N - 1;              // steps per sweep
-  constexpr int LD = N + 1;
-  constexpr int GPW = SVDJ_WAVE / W;    // row groups per wave
-  constexpr int NGRP = NWAVE * GPW;     // row groups
-  constexpr int RPL = N / NGRP;         // Q rows per lane
-  static_assert(N % NGRP == 0, "rows must split evenly over row groups");
+  constexpr int NTRI = N * (N - 1) / 2;
+  constexpr int GPW = SVDJ_WAVE / W;    // Q row groups per wave
+  constexpr int NGRP = (NWAVE - 1) * GPW;  // Q row groups (waves 1..NWAVE-1)
+  constexpr int RPL = (N + NGRP - 1) / NGRP;  // Q rows per lane (the last group may idle)
+  constexpr int MAXOFF = EvdDeal<W, NT>::MAXOFF;
+  static_assert(W >= 4 && W <= 64 && NWAVE >= 2, "EVD geometry");
+#ifdef SVDJ_EVD_Q32
+  using QT = T;
+#else
+  using QT = double;
+#endif
+  static constexpr EvdDeal<W, NT> deal{};
 
-  __shared__ T G[N * LD];
-  // rotation records, double-buffered by global step parity (structure of
-  // arrays: consecutive slots on consecutive banks)
-  __shared__ T rc[2][W], rs[2][W], rt[2][W], rdp[2][W], rdq[2][W];
-  __shared__ int rot_flag[2];  // any rotation in sweep (parity)
+  __shared__ T Gb[2][NTRI + 1];  // off-diagonal G by position pair, double-buffered;
+                                 // element NTRI takes the writes that go nowhere
+  __shared__ T dg[N];        // assembled diagonal (player order)
+  // rotation records by global step parity (structure of arrays): (c, s) in
+  // the data precision steer G, (cq, sq) in the Q precision rotate Q (fp64
+  // for fp32 data: normalised once, by the solver), (dp, dq) are the slot's
+  // diagonals after its rotation
+  __shared__ T rc[2][W], rs[2][W], rdp[2][W], rdq[2][W];
+  __shared__ QT rcq[2][W], rsq[2][W];
+  __shared__ int rot_flag[2];  // any rotation in sweep (parity), written by wave 0
   __shared__ float wmax[NWAVE];
   __shared__ int wneed[NWAVE];
-  __shared__ float pair_max;
   __shared__ int need_any;
 
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  EVD_T(9);
 
-  // ---- assemble G (split-K slabs summed in fp64, then rounded once)
+  // ---- assemble G: diagonal first (player order), then every off-diagonal
+  // entry into position space for step 0; split-K slabs summed in fp64
   if (full) {
     const T* s0 = slabs + (size_t)pair * nchunk * (4 * W * W);
-    for (int i = tid; i < N * N; i += NT) {
+    for (int a = tid; a < N; a += NT) {
       double acc = 0;
-#pragma unroll 4
-      for (int c = 0; c < nchunk; ++c) acc += (double)s0[(size_t)c * 4 * W * W + i];
-      G[(i / N) * LD + (i % N)] = (T)acc;
+      for (int c = 0; c < nchunk; ++c) acc += (double)s0[(size_t)c * 4 * W * W + a * N + a];
+      dg[a] = (T)acc;
     }
   } else {
-    const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
-    for (int i = tid; i < N * N; i += NT) G[(i / N) * LD + (i % N)] = T(0);
-    __syncthreads();
-    for (int i = tid; i < W * W; i += NT) {
-      double acc = 0;
-#pragma unroll 4
-      for (int c = 0; c < nchunk; ++c) acc += (double)s0[(size_t)c * W * W + i];
-      const int a = i / W, b = i % W;
-      G[a * LD + W + b] = (T)acc;
-      G[(W + b) * LD + a] = (T)acc;
-    }
-    for (int a = tid; a < W; a += NT) {
-      G[a * LD + a] = D[bi * W + a];
-      G[(W + a) * LD + W + a] = D[bj * W + a];
-    }
+    for (int a = tid; a < N; a += NT) dg[a] = D[a < W ? bi * W + a : bj * W + (a - W)];
   }
-  if (tid == 0) rot_flag[0] = rot_flag[1] = 0;
   __syncthreads();
-
-  // ---- convergence value before any rotation, and whether any pair would
-  // rotate at all (same test as the solve: if none does, the first pass
-  // rotates nothing -- G never changes -- so it is skipped exactly)
   {
     float mx = 0.0f;
     int need = 0;
-    for (int i = tid; i < N * N; i += NT) {
-      const int r = i / N, c = i % N;
-      const bool use = full ? (r < c) : (r < W && c >= W);
-      if (!use) continue;
-      const T grr = G[r * LD + r], gcc = G[c * LD + c], grc = G[r * LD + c];
+    // store an entry at its step-0 position; fold it into the convergence
+    // value and the "anything to rotate" test
+    auto visit = [&](int r, int c, T g) {
+      Gb[0][tri_idx<N>(pos0<W>(r), pos0<W>(c))] = g;
+      const T grr = dg[r], gcc = dg[c];
       const T d = sqrt(grr) * sqrt(gcc);
       if (d > T(0)) {
-        const float v = (float)(fabs(grc) / d);
+        const float v = (float)(fabs(g) / d);
         mx = v > mx ? v : mx;
       }
-      need |= needs_rotation(grr, gcc, grc, tol, absmode) ? 1 : 0;
+      need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
+    };
+    // Slab sums with 16-byte loads, all chunks of a group in flight at once
+    // (one dependent global load per entry and chunk was ~12 us per kernel).
+    constexpr int EV = 16 / (int)sizeof(T);
+    if (full) {
+      const T* s0 = slabs + (size_t)pair * nchunk * (4 * W * W);
+      for (int gi = tid; gi < N * N / EV; gi += NT) {
+        double acc[EV];
+#pragma unroll
+        for (int u = 0; u < EV; ++u) acc[u] = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < nchunk; ++k) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)k * 4 * W * W + gi * EV);
+          const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+          for (int u = 0; u < EV; ++u) acc[u] += (double)e[u];
+        }
+#pragma unroll
+        for (int u = 0; u < EV; ++u) {
+          const int i = gi * EV + u, r = i / N, c = i % N;
+          if (r < c) visit(r, c, (T)acc[u]);
+        }
+      }
+    } else {
+      // couplings inside a block are zero (blocks are kept internally orthogonal)
+      for (int i = tid; i < N * N; i += NT) {
+        const int r = i / N, c = i % N;
+        if (r < c && (c < W || r >= W)) Gb[0][tri_idx<N>(pos0<W>(r), pos0<W>(c))] = T(0);
+      }
+      const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
+      for (int gi = tid; gi < W * W / EV; gi += NT) {
+        double acc[EV];
+#pragma unroll
+        for (int u = 0; u < EV; ++u) acc[u] = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < nchunk; ++k) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)k * W * W + gi * EV);
+          const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+          for (int u = 0; u < EV; ++u) acc[u] += (double)e[u];
+        }
+#pragma unroll
+        for (int u = 0; u < EV; ++u) {
+          const int i = gi * EV + u;
+          visit(i / W, W + i % W, (T)acc[u]);
+        }
+      }
     }
     mx = wave_max(mx);
     need = __any(need) ? 1 : 0;
@@ -384,173 +549,197 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         n2 |= wneed[w];
       }
       atomic_max_pos(&metric[0], m2);
-      pair_max = m2;
       need_any = n2;
     }
     __syncthreads();
   }
+  // If no pair passes the rotation test, the first pass would rotate nothing
+  // (G never changes): it is skipped exactly.
   const bool run = need_any != 0;
 
-  // ---- off-diagonal slot-pair blocks (a < b) owned by this thread, dealt
-  // round robin over the strict upper triangle in rows taken in
-  // complementary pairs 0, W-2, 1, W-3, ...: a pair of rows is W blocks, so
-  // a 32-lane LDS group spans fewer row boundaries, where G's bank
-  // (p + r) mod 32 repeats.
-  constexpr int NOFF = W * (W - 1) / 2;
-  constexpr int MAXOFF = (NOFF + NT - 1) / NT;
+  // ---- this thread's blocks and their static addresses
   int ba[MAXOFF], bb[MAXOFF];
+  int rd[MAXOFF][4], wr[MAXOFF][4];  // read / write element index (NTRI: no write)
+  int pw = NTRI, sv = -1;  // solve duty (256*e + meeting; j = 0 only) and its pending address
 #pragma unroll
   for (int j = 0; j < MAXOFF; ++j) {
-    const int idx = tid + j * NT;
+    const int code = deal.blk[j * NT + tid];
     ba[j] = bb[j] = -1;
-    if (idx < NOFF) {
-      int i = 0, base = 0, a = 0;
-      for (;; ++i) {
-        a = (i & 1) ? W - 2 - (i >> 1) : (i >> 1);
-        if (idx < base + (W - 1 - a)) break;
-        base += W - 1 - a;
-      }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rd[j][e] = wr[j][e] = 0;
+    if (code != 0xffff) {
+      const int a = code >> 8, b = code & 255;
       ba[j] = a;
-      bb[j] = a + 1 + (idx - base);
+      bb[j] = b;
+      const int pa[2] = {slot_first_pos<W>(a), slot_second_pos<W>(a)};
+      const int pb[2] = {slot_first_pos<W>(b), slot_second_pos<W>(b)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int x = pa[e >> 1], y = pb[e & 1];
+        rd[j][e] = tri_idx<N>(x, y);
+        wr[j][e] = tri_idx<N>(pos_next<W>(x), pos_next<W>(y));
+        if (j == 0 && tid < W) {
+          const int mt = next_meeting<W>(x, y);
+          if (mt >= 0) {
+            wr[j][e] = NTRI;  // a within-slot entry next step: written one phase later
+            pw = tri_idx<N>(pos_next<W>(pos_next<W>(x)), pos_next<W>(pos_next<W>(y)));
+            sv = 256 * e + mt;
+          }
+        }
+      }
     }
   }
+  T pend = T(0);
 
-  // ---- slot layout state of the register Q
+  // ---- slot layout state of the register Q (waves 1..NWAVE-1)
+  const bool qlane = wave > 0;
   const int slot = lane % W;
-  const int grp = wave * GPW + lane / W;
+  const int grp = (wave - 1) * GPW + lane / W;
   int pf = slot == 0 ? N - 1 : slot;          // first player of this slot
   int ps = slot == 0 ? 0 : N - 1 - slot;      // second player
-  double qf[RPL], qs[RPL];
+  QT qf[RPL], qs[RPL];
 #pragma unroll
   for (int i = 0; i < RPL; ++i) {
     const int k = grp * RPL + i;
-    qf[i] = (k == pf) ? 1.0 : 0.0;
-    qs[i] = (k == ps) ? 1.0 : 0.0;
+    qf[i] = (k == pf) ? QT(1) : QT(0);
+    qs[i] = (k == ps) ? QT(1) : QT(0);
   }
-  auto sidx = [](int i, int j) { return i < j ? i * LD + j : j * LD + i; };
 
-  // ---- prologue: the rotations of step 0 from the assembled G
+  // ---- prologue: step 0's rotations from the assembled G
+  auto publish = [&](int b, int ns, T c, T sn, T t, T dfp, T dsp) {
+    rc[b][ns] = c;
+    rs[b][ns] = sn;
+    rdp[b][ns] = dfp;
+    rdq[b][ns] = dsp;
+    if constexpr (sizeof(QT) == sizeof(T)) {
+      rcq[b][ns] = c;
+      rsq[b][ns] = sn;
+    } else {  // fp64 (c, s) of the fp32 t, normalised in fp64
+      const double td = (double)t, c64 = rsqrt64(fma(td, td, 1.0));
+      rcq[b][ns] = c64;
+      rsq[b][ns] = td * c64;
+    }
+  };
+  // rotations seen by this solver lane in the current / next inner sweep
+  // (OR-reduced over wave 0 once per sweep: no per-step flag store)
+  int racc = 0, racc_next = 0;
   if (run && tid < W) {
+    const int fa = slot_first_pos<W>(tid), sa = slot_second_pos<W>(tid);
     int p, q;
     ring_slot<W>(tid, 0, p, q);
-    const int ipq = sidx(p, q);
-    const T gpp = G[p * LD + p], gqq = G[q * LD + q], gpq = G[ipq];
-    T c = 1, s = 0, t = 0, dp = gpp, dq = gqq;
-    if (rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t)) {
-      dp = gpp - t * gpq;
-      dq = gqq + t * gpq;
-      G[ipq] = T(0);
-      rot_flag[0] = 1;
-    }
-    rc[0][tid] = c;
-    rs[0][tid] = s;
-    rt[0][tid] = t;
-    rdp[0][tid] = dp;
-    rdq[0][tid] = dq;
+    const T gpp = dg[p], gqq = dg[q];
+    const T gpq = Gb[0][tri_idx<N>(fa, sa)];
+    T c, s, t;
+    const bool rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
+    racc = rot;
+    // thread tid's duty block holds next-step slot tid (EvdDeal), so phase 0's
+    // pending write moves this coupling to its step-1 position
+    pend = rot ? T(0) : gpq;
+    publish(0, tid, c, s, t, gpp - t * gpq, gqq + t * gpq);
   }
+  EVD_T(8);
+  EVD_ACC(4, 9, 8);
   __syncthreads();
 
+  // One block's update J^T G J (entries moved to their next-step positions)
+  // and, for a duty block, the next step's rotation of its slot.
+  auto update_block = [&](int j, int b, int nb, bool duty, bool last) {
+    const T* __restrict__ Gr = Gb[b];
+    T* __restrict__ Gw = Gb[nb];
+    // the coupling of this step's pair, solved last phase (or in the
+    // prologue), moved on to its next-step position (dummy if no duty)
+    if (j == 0) Gw[pw] = pend;
+    // every LDS read of the block up front (static addresses)
+    const T g00 = Gr[rd[j][0]], g01 = Gr[rd[j][1]], g10 = Gr[rd[j][2]], g11 = Gr[rd[j][3]];
+    const T ca = rc[b][ba[j]], sa = rs[b][ba[j]], cb = rc[b][bb[j]], sb = rs[b][bb[j]];
+    T dx = T(0), dy = T(0);
+    const int e = sv >> 8;
+    if (duty) {
+      dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
+      dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
+    }
+    const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
+    const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
+    const T h[4] = {cb * h00 - sb * h01, sb * h00 + cb * h01, cb * h10 - sb * h11,
+                    sb * h10 + cb * h11};
+    if (duty) {
+      const int ns = (sv & 255) >> 1;
+      const bool x_first = sv & 1;
+      const T g = e == 0 ? h[0] : e == 1 ? h[1] : e == 2 ? h[2] : h[3];
+      const T df = x_first ? dx : dy, ds = x_first ? dy : dx;
+      T c, sn, t;
+      const bool rot = rotation_fast(df, ds, g, tol, absmode, c, sn, t);
+      if (last) racc_next |= rot; else racc |= rot;
+      pend = rot ? T(0) : g;
+      publish(nb, ns, c, sn, t, df - t * g, ds + t * g);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Gw[wr[j][q]] = h[q];
+  };
+
   bool any = false;
-  int gs = 0;  // global step counter: records of step gs live in buffer gs & 1
+  int gs = 0;  // global step counter: step gs reads buffer gs & 1, records gs & 1
   for (int sw = 0; sw < (run ? max_inner : 0); ++sw) {
     for (int st = 0; st < R; ++st, ++gs) {
       EVD_T(0);
       const int b = gs & 1, nb = b ^ 1;
-      const int stn = st + 1 == R ? 0 : st + 1;      // next step (of this or the next sweep)
-      const int nflag = (st + 1 == R ? sw + 1 : sw) & 1;
-      if (sw >= 1 && st == 1 && tid == 0) rot_flag[(sw + 1) & 1] = 0;  // read by all by now
-      // G <- J^T G J on this thread's blocks, and the next step's solves
+      const bool last = st + 1 == R;  // this phase solves step 0 of the next sweep
+      if (wave == 0) {
+        // solver wave: its duty blocks (lanes < W, j = 0) and nothing else of Q
 #pragma unroll
-      for (int j = 0; j < MAXOFF; ++j) {
-        if (ba[j] < 0) continue;
-        int p, q, r, u;
-        ring_slot<W>(ba[j], st, p, q);
-        ring_slot<W>(bb[j], st, r, u);
-        const int idx[4] = {sidx(p, r), sidx(p, u), sidx(q, r), sidx(q, u)};
-        const T g00 = G[idx[0]], g01 = G[idx[1]], g10 = G[idx[2]], g11 = G[idx[3]];
-        const T ca = rc[b][ba[j]], sa = rs[b][ba[j]], cb = rc[b][bb[j]], sb = rs[b][bb[j]];
-        const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
-        const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
-        T h[4] = {cb * h00 - sb * h01, sb * h00 + cb * h01, cb * h10 - sb * h11,
-                  sb * h10 + cb * h11};
-        // next-step placement of the four players
-        const int wp = ring_where<W>(p, stn), wq = ring_where<W>(q, stn);
-        const int wr = ring_where<W>(r, stn), wu = ring_where<W>(u, stn);
-        const int wx[4] = {wp, wp, wq, wq}, wy[4] = {wr, wu, wr, wu};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if ((wx[e] >> 1) == (wy[e] >> 1)) {
-            // (x, y) rotate together next step: x from slot ba (role by e>>1),
-            // y from slot bb (role by e&1); post-step-st diagonals from the records
-            const T dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
-            const T dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
-            const bool x_first = wx[e] & 1;
-            const T df = x_first ? dx : dy, ds = x_first ? dy : dx;
-            const int ns = wx[e] >> 1;
-            T c = 1, s = 0, t = 0, dfp = df, dsp = ds;
-            if (rotation_fast(df, ds, h[e], tol, absmode, c, s, t)) {
-              dfp = df - t * h[e];
-              dsp = ds + t * h[e];
-              h[e] = T(0);
-              rot_flag[nflag] = 1;
-            }
-            rc[nb][ns] = c;
-            rs[nb][ns] = s;
-            rt[nb][ns] = t;
-            rdp[nb][ns] = dfp;
-            rdq[nb][ns] = dsp;
-          }
-          G[idx[e]] = h[e];
+        for (int j = 0; j < MAXOFF; ++j)
+          if (ba[j] >= 0) update_block(j, b, nb, j == 0 && sv >= 0, last);
+        if (last) {  // every rotation of sweep sw is decided by now
+          const int rot = __any(racc) ? 1 : 0;
+          if (lane == 0) rot_flag[sw & 1] = rot;
+          racc = racc_next;
+          racc_next = 0;
         }
-      }
-      EVD_T(1);
-      // Q <- Q J in registers (fp64): (c, s) of step st from t, normalised in fp64
-      {
-        const T tq = rt[b][slot];
-        if (tq != T(0)) {
-          double c64, s64;
-          if constexpr (sizeof(T) == 8) {
-            c64 = rc[b][slot];
-            s64 = rs[b][slot];
-          } else {
-            const double td = (double)tq;
-            c64 = rsqrt64(1.0 + td * td);
-            s64 = td * c64;
-          }
+        EVD_T(1);
+        EVD_T(2);
+        EVD_ACC(1, 1, 2);
+        EVD_ACC(0, 0, 1);
+      } else {
+        // Q waves: this step's Q rotation (records read up front)
+        const QT cq = rcq[b][slot], sq = rsq[b][slot];
 #pragma unroll
-          for (int i = 0; i < RPL; ++i) {
-            const double x = qf[i], y = qs[i];
-            qf[i] = c64 * x - s64 * y;
-            qs[i] = s64 * x + c64 * y;
-          }
+        for (int j = 0; j < MAXOFF; ++j)
+          if (ba[j] >= 0) update_block(j, b, nb, false, last);
+        EVD_T(1);
+        // Q <- Q J in registers (c = 1, s = 0 for no rotation)
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+          const QT x = qf[i], y = qs[i];
+          qf[i] = cq * x - sq * y;
+          qs[i] = sq * x + cq * y;
         }
-      }
-      // advance the round robin: firsts shift right, seconds shift left
+        // advance the round robin: firsts shift right, seconds shift left
 #pragma unroll
-      for (int i = 0; i < RPL; ++i) {
-        const double f_r = dpp_shr1(qf[i]), s_r = dpp_shr1(qs[i]), s_l = dpp_shl1(qs[i]);
-        const double nf = slot == 0 ? qf[i] : (slot == 1 ? s_r : f_r);
-        const double ns = slot == W - 1 ? qf[i] : s_l;
-        qf[i] = nf;
-        qs[i] = ns;
-      }
-      {
+        for (int i = 0; i < RPL; ++i) {
+          const QT f_r = dpp_shr1(qf[i]), s_r = dpp_shr1(qs[i]), s_l = dpp_shl1(qs[i]);
+          const QT nf = slot == 0 ? qf[i] : (slot == 1 ? s_r : f_r);
+          const QT ns = slot == W - 1 ? qf[i] : s_l;
+          qf[i] = nf;
+          qs[i] = ns;
+        }
         const int f_r = dpp_shr1(pf), s_r = dpp_shr1(ps), s_l = dpp_shl1(ps);
         const int nf = slot == 0 ? pf : (slot == 1 ? s_r : f_r);
         const int ns = slot == W - 1 ? pf : s_l;
         pf = nf;
         ps = ns;
+        EVD_T(2);
+        EVD_ACC(0, 0, 1);
+        EVD_ACC(1, 1, 2);
       }
-      EVD_T(2);
       __syncthreads();
       EVD_T(3);
-      EVD_ACC(0, 0, 1);
-      EVD_ACC(1, 1, 2);
-      EVD_ACC(2, 2, 3);
+      EVD_ACC(2, 0, 3);
     }
     if (!rot_flag[sw & 1]) break;
     any = true;
   }
+  EVD_T(7);
+  EVD_ACC(5, 8, 7);
 
   if (tid == 0) {
     skip[pair] = any ? 0 : 1;
@@ -559,12 +748,16 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   // Full mode re-measured the diagonal from the data: always refresh D.
   if (!any && !full) return;
   if (any) {
-    T* qo = Qout + (size_t)pair * N * N;
+    if (qlane) {
+      T* qo = Qout + (size_t)pair * N * N;
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-      const int k = grp * RPL + i;
-      qo[k * N + pf] = (T)qf[i];
-      qo[k * N + ps] = (T)qs[i];
+      for (int i = 0; i < RPL; ++i) {
+        const int k = grp * RPL + i;
+        if (k < N) {
+          qo[k * N + pf] = (T)qf[i];
+          qo[k * N + ps] = (T)qs[i];
+        }
+      }
     }
     // diagonals after the last executed step (records of step gs - 1)
     if (tid < W) {
@@ -575,8 +768,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       D[q < W ? bi * W + q : bj * W + (q - W)] = rdq[lb][tid];
     }
   } else {
-    for (int a = tid; a < N; a += NT)
-      D[a < W ? bi * W + a : bj * W + (a - W)] = G[a * LD + a];
+    for (int a = tid; a < N; a += NT) D[a < W ? bi * W + a : bj * W + (a - W)] = dg[a];
   }
 }
 
@@ -941,7 +1133,8 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
 template <typename T, int W>
-static int launch_gram_evd(const Chain<T>& c, int s, double tol, int max_inner, uint32_t* metric) {
+static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, int max_inner,
+                           uint32_t* metric) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
   const int full = c.modes ? c.modes[s] : 0;
@@ -952,8 +1145,9 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int max_inner, 
     hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
                        c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   SVDJ_LAUNCH_CHECK();
-    hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
-                       c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, max_inner, metric);
+  hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
+                     c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode, max_inner,
+                     metric);
   SVDJ_LAUNCH_CHECK();
   return 0;
 }
@@ -996,9 +1190,10 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
 // (a dominant column, or Q ~ I late in the iteration): on U(0,1) 8192^2 the
 // final ||AV - US||/||A|| is 6.5e-4 vs 8e-6 native.  Native is the default.
 template <typename T, int W>
-static int block_steps_t(const Chain<T>& c, double tol, int max_inner, uint32_t* metric, int mma) {
+static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inner,
+                         uint32_t* metric, int mma) {
   for (int s = 0; s < c.steps; ++s) {
-    int rc = launch_gram_evd<T, W>(c, s, tol, max_inner, metric);
+    int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric);
     if (!rc) rc = launch_apply<T, W>(c, s, mma);
     if (rc) return rc;
   }
@@ -1049,8 +1244,8 @@ static hipEvent_t* stagger_events(hipStream_t rec, hipStream_t wait, int& n) {
 // which matters when the per-GPU work is small (many GPUs): the EVD latency
 // is then the critical path (tools/gpu_latency_sim.sh, tools/trace_gaps.py).
 template <typename T, int W>
-static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int max_inner,
-                          uint32_t* metric, int mma) {
+static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int absmode,
+                          int max_inner, uint32_t* metric, int mma) {
   int ne = 0;
   hipEvent_t* ev = stagger_events(a.st, b.st, ne);
   if (!ev) {
@@ -1061,13 +1256,13 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
   for (int s = 0; s < n; ++s) {
     int rc = 0;
     if (s < a.steps) {
-      rc = launch_gram_evd<T, W>(a, s, tol, max_inner, metric);
+      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
       if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
       if (!rc) rc = launch_apply<T, W>(a, s, mma);
     }
     if (!rc && s < b.steps) {
       if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, max_inner, metric);
+      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric);
       if (!rc) rc = launch_apply<T, W>(b, s, mma);
     }
     if (rc) {
@@ -1116,14 +1311,16 @@ static int check_dims(int m_pad, int lda, const void* V, int n_v, int ldv, int m
 template <typename T, int W>
 static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D,
                           const int32_t* pairs, int P, int steps, const int32_t* modes,
-                          double tol, int max_inner, void* ws, size_t ws_bytes, uint32_t* metric,
-                          int mma, void* stream, const int32_t* pairs2, int P2, int steps2,
-                          const int32_t* modes2, void* ws2, size_t ws2_bytes, void* stream2) {
+                          double tol, int absmode, int max_inner, void* ws, size_t ws_bytes,
+                          uint32_t* metric, int mma, void* stream, const int32_t* pairs2, int P2,
+                          int steps2, const int32_t* modes2, void* ws2, size_t ws2_bytes,
+                          void* stream2) {
   Chain<T> a, b;
   int rc = chain_init<T, W>(a, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
                             ws, ws_bytes, mma, (hipStream_t)stream);
   if (rc) return rc;
-  if (!pairs2 || P2 <= 0 || steps2 <= 0) return block_steps_t<T, W>(a, tol, max_inner, metric, mma);
+  if (!pairs2 || P2 <= 0 || steps2 <= 0)
+    return block_steps_t<T, W>(a, tol, absmode, max_inner, metric, mma);
   if (ws2 == ws || stream2 == stream) {
     set_error("staggered chains need distinct workspaces and streams");
     return -2;
@@ -1131,20 +1328,25 @@ static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv
   rc = chain_init<T, W>(b, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs2, P2, steps2, modes2,
                         ws2, ws2_bytes, mma, (hipStream_t)stream2);
   if (rc) return rc;
-  return block_steps2_t<T, W>(a, b, tol, max_inner, metric, mma);
+  return block_steps2_t<T, W>(a, b, tol, absmode, max_inner, metric, mma);
 }
 
 static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v, int ldv,
                      void* D, const int32_t* pairs, int P, int steps, const int32_t* modes,
-                     double tol, int max_inner, void* ws, size_t ws_bytes, uint32_t* metric,
-                     int mma, void* stream, const int32_t* pairs2, int P2, int steps2,
-                     const int32_t* modes2, void* ws2, size_t ws2_bytes, void* stream2) {
+                     double tol, int tol_mode, int max_inner, void* ws, size_t ws_bytes,
+                     uint32_t* metric, int mma, void* stream, const int32_t* pairs2, int P2,
+                     int steps2, const int32_t* modes2, void* ws2, size_t ws2_bytes,
+                     void* stream2) {
   int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
   if (rc) return rc;
+  if (tol_mode != 0 && tol_mode != 1) {
+    set_error("bad tol_mode %d (0 relative, 1 absolute)", tol_mode);
+    return -2;
+  }
   if (P <= 0 || steps < 0) return 0;
 #define SVDJ_STEPS_ARGS                                                                       \
-  m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol, max_inner, ws, ws_bytes, metric, \
-      mma, stream, pairs2, P2, steps2, modes2, ws2, ws2_bytes, stream2
+  m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol, tol_mode, max_inner, ws, ws_bytes, \
+      metric, mma, stream, pairs2, P2, steps2, modes2, ws2, ws2_bytes, stream2
   if (dtype == 0 && W == 32) return steps_dispatch<float, 32>(SVDJ_STEPS_ARGS);
   if (dtype == 0 && W == 64) return steps_dispatch<float, 64>(SVDJ_STEPS_ARGS);
   if (dtype == 1 && W == 32) return steps_dispatch<double, 32>(SVDJ_STEPS_ARGS);
@@ -1155,11 +1357,12 @@ static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int
 
 extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                 int ldv, void* D, const int32_t* pairs, int P, int steps,
-                                const int32_t* modes, double tol, int max_inner, void* ws,
-                                size_t ws_bytes, uint32_t* metric, int mma, void* stream) {
+                                const int32_t* modes, double tol, int tol_mode, int max_inner,
+                                void* ws, size_t ws_bytes, uint32_t* metric, int mma,
+                                void* stream) {
   return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
-                   max_inner, ws, ws_bytes, metric, mma, stream, nullptr, 0, 0, nullptr, nullptr,
-                   0, nullptr);
+                   tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, nullptr, 0, 0, nullptr,
+                   nullptr, 0, nullptr);
 }
 
 extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
@@ -1167,16 +1370,16 @@ extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, 
                                  const int32_t* modes, void* ws, size_t ws_bytes, void* stream,
                                  const int32_t* pairs2, int P2, int steps2, const int32_t* modes2,
                                  void* ws2, size_t ws2_bytes, void* stream2, double tol,
-                                 int max_inner, uint32_t* metric, int mma) {
+                                 int tol_mode, int max_inner, uint32_t* metric, int mma) {
   return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
-                   max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2, modes2, ws2,
-                   ws2_bytes, stream2);
+                   tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2,
+                   modes2, ws2, ws2_bytes, stream2);
 }
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
-                                int ldv, void* D, int ncols, double tol, int max_inner,
-                                int max_sweeps, void* ws, size_t ws_bytes, uint32_t* metric,
-                                double* hist, int mma, void* stream) {
+                                int ldv, void* D, int ncols, double tol, int tol_mode,
+                                int max_inner, int max_sweeps, void* ws, size_t ws_bytes,
+                                uint32_t* metric, double* hist, int mma, void* stream) {
   if (W <= 0 || ncols % W) {
     set_error("ncols %d not a multiple of W %d", ncols, W);
     return -2;
@@ -1210,7 +1413,8 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   for (int sw = 0; sw < max_sweeps; ++sw) {
     if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
     rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,
-                          modes.data(), tol, max_inner, ws, ws_bytes, metric, mma, stream);
+                          modes.data(), tol, tol_mode, max_inner, ws, ws_bytes, metric, mma,
+                          stream);
     if (rc) break;
     if (hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {

@@ -60,6 +60,8 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   pairs   device int32 [steps][P][2] block indices
 //   modes   host   int32 [steps] (0 cross / 1 full), NULL = all cross
 //   metric  device uint32[2] as for the scalar path.
+//   tol_mode 0: rotate when |g_pq| > tol sqrt(g_pp g_qq) (relative, default);
+//            1: when |g_pq| > tol (the reference's absolute TOLERANCE test).
 //   mma     matrix-core mode: 0 native (f32 / f64 MFMA), 1 fp32 data on bf16
 //           MFMA with a 3-way bf16 split (6 products, fp32-level accuracy),
 //           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
@@ -67,7 +69,7 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
 int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, const int32_t* pairs, int P,
-                     int steps, const int32_t* modes, double tol,
+                     int steps, const int32_t* modes, double tol, int tol_mode,
                      int max_inner_sweeps, void* workspace, size_t ws_bytes,
                      uint32_t* metric, int mma, void* stream);
 
@@ -81,13 +83,13 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
                       size_t ws_bytes, void* stream, const int32_t* pairs2,
                       int P2, int steps2, const int32_t* modes2,
                       void* workspace2, size_t ws2_bytes, void* stream2,
-                      double tol, int max_inner_sweeps, uint32_t* metric,
-                      int mma);
+                      double tol, int tol_mode, int max_inner_sweeps,
+                      uint32_t* metric, int mma);
 
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode.  Returns sweeps, <0 on error.
 int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
-                     int n_v, int ldv, void* D, int ncols, double tol,
+                     int n_v, int ldv, void* D, int ncols, double tol, int tol_mode,
                      int max_inner_sweeps, int max_sweeps, void* workspace,
                      size_t ws_bytes, uint32_t* metric, double* hist,
                      int mma, void* stream);

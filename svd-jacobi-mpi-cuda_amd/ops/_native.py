@@ -108,15 +108,16 @@ def hip_lib():
         _sig(lib, "svdj_block_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int])
         _sig(lib, "svdj_block_steps", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
-              c_int, c_int, c_i32_p, c_double, c_int, c_void_p, c_size_t, c_void_p, c_int,
+              c_int, c_int, c_i32_p, c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_int,
               c_void_p])
         _sig(lib, "svdj_block_steps2", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
               c_int, c_int, c_i32_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_int,
-              c_i32_p, c_void_p, c_size_t, c_void_p, c_double, c_int, c_void_p, c_int])
+              c_i32_p, c_void_p, c_size_t, c_void_p, c_double, c_int, c_int, c_void_p, c_int])
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
-              c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int, c_void_p])
+              c_double, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
+              c_void_p])
         _sig(lib, "svdj_apply_q", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,

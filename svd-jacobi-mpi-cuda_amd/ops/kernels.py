@@ -42,6 +42,17 @@ def mma_code(mma: str | int, dtype: torch.dtype) -> int:
     return MMA_CODES[mma]
 
 
+def tol_mode_code(tol_mode) -> int:
+    """0 = relative |g_pq| > tol sqrt(g_pp g_qq) (default), 1 = absolute
+    |g_pq| > tol (the reference's TOLERANCE test, lib/global.cuh:9)."""
+    if tol_mode in (0, 1):
+        return int(tol_mode)
+    table = {"relative": 0, "absolute": 1}
+    if tol_mode not in table:
+        raise ValueError(f"bad tol_mode {tol_mode!r}; 'relative' or 'absolute'")
+    return table[tol_mode]
+
+
 def dtype_code(dtype: torch.dtype) -> int:
     if dtype == torch.float32:
         return 0
@@ -210,7 +221,7 @@ def check_block(dtype, W):
 
 
 def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0,
-                mma="native", pool: dict | None = None):
+                mma="native", pool: dict | None = None, tol_mode="relative"):
     """Run ``len(modes)`` block steps on the current stream.  pairs: int32
     (steps, P, 2) on At's device (block indices local to At); modes: list of
     0 (cross) / 1 (full).  Chains running concurrently on different streams
@@ -227,18 +238,19 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
         ldv = Vt.stride(0) if Vt is not None else 0
         hip_check(hip_lib().svdj_block_steps(
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
-            _ptr(D), _ptr(pairs), P, steps, md, float(tol), int(max_inner), _ptr(ws),
-            ws.numel(), _ptr(metric), mma_code(mma, At.dtype), _stream(At)), "block_steps")
+            _ptr(D), _ptr(pairs), P, steps, md, float(tol), tol_mode_code(tol_mode),
+            int(max_inner), _ptr(ws), ws.numel(), _ptr(metric), mma_code(mma, At.dtype),
+            _stream(At)), "block_steps")
     else:
         for s in range(steps):
             mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, bool(modes[s]), tol,
-                                      max_inner)
+                                      max_inner, tol_mode=tol_mode_code(tol_mode))
             metric[0] = max(float(metric[0]), mx)
             metric[1] += nrot
 
 
 def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native",
-                 pool: dict | None = None):
+                 pool: dict | None = None, tol_mode="relative"):
     """Two independent chains of block steps, staggered (svdj_block_steps2).
     ``chain_x = (pairs, modes, ws_slot, stream)``: device pairs (steps, P, 2),
     host modes, a workspace slot and the torch stream of that chain.  Step s
@@ -246,7 +258,8 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     the chains run one after the other."""
     if not At.is_cuda:
         for pairs, modes, slot, _ in (chain_a, chain_b):
-            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool)
+            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool,
+                        tol_mode)
         return
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
@@ -261,8 +274,8 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     ldv = Vt.stride(0) if Vt is not None else 0
     hip_check(hip_lib().svdj_block_steps2(
         dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
-        *args[0], *args[1], float(tol), int(max_inner), _ptr(metric), mma_code(mma, At.dtype)),
-        "block_steps2")
+        *args[0], *args[1], float(tol), tol_mode_code(tol_mode), int(max_inner), _ptr(metric),
+        mma_code(mma, At.dtype)), "block_steps2")
 
 
 def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
@@ -275,7 +288,8 @@ def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
                                      rows, Xt.stride(0), _ptr(Q), _stream(Xt)), "apply_q")
 
 
-def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
+def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
+                tol_mode="relative"):
     """Single-device block Jacobi (round-robin over ncols/W blocks, first
     step of each sweep full).  Returns (sweeps, hist)."""
     _check_layout(At, m_pad)
@@ -290,8 +304,9 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
         ldv = Vt.stride(0) if Vt is not None else 0
         sweeps = hip_check(hip_lib().svdj_block_solve(
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
-            ncols, float(tol), int(max_inner), int(max_sweeps), _ptr(ws), ws.numel(),
-            _ptr(metric), hist, mma_code(mma, At.dtype), _stream(At)), "block_solve")
+            ncols, float(tol), tol_mode_code(tol_mode), int(max_inner), int(max_sweeps),
+            _ptr(ws), ws.numel(), _ptr(metric), hist, mma_code(mma, At.dtype), _stream(At)),
+            "block_solve")
         return sweeps, [hist[i] for i in range(sweeps)]
     from ..parallel.schedule import round_robin
 
@@ -301,7 +316,8 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native"):
     hist = []
     for _ in range(max_sweeps):
         metric = new_metric("cpu")
-        block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric)
+        block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric,
+                    tol_mode=tol_mode)
         mx, nrot = read_metric(metric)
         hist.append(mx)
         if nrot == 0:

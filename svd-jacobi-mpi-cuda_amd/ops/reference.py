@@ -77,7 +77,7 @@ def round_robin_pairs(N):
 _RR_CACHE = {}
 
 
-def jacobi_evd(G, tol, max_sweeps):
+def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0):
     """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
 
     Same round-robin ordering, threshold and update formulas as the LDS
@@ -97,7 +97,7 @@ def jacobi_evd(G, tol, max_sweeps):
         for p, q in sched:
             gpp, gqq, gpq = G[:, p, p], G[:, q, q], G[:, p, q]
             nrm = gpp.clamp(min=0).sqrt() * gqq.clamp(min=0).sqrt()
-            rot = (nrm > 0) & (gpq.abs() > tol * nrm)
+            rot = (gpq.abs() > tol) if tol_mode == 1 else (nrm > 0) & (gpq.abs() > tol * nrm)
             if not bool(rot.any()):
                 continue
             sweep_rot |= rot.any(1)
@@ -125,7 +125,7 @@ def jacobi_evd(G, tol, max_sweeps):
     return torch.diagonal(G, dim1=1, dim2=2).clone(), Q, rotated
 
 
-def block_step(At, Vt, D, pairs, W, full, tol, max_inner):
+def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0):
     """One block step on P disjoint block pairs (pairs: (P, 2) block ids).
 
     Mirrors csrc/hip/block.hip (gram -> evd -> apply).  Updates At, Vt, D in
@@ -156,7 +156,7 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner):
     den = dg[:, :, None] * dg[:, None, :]
     R = torch.where(den > 0, G.abs() / torch.where(den > 0, den, torch.ones_like(den)), torch.zeros_like(den))
     maxconv = float(R[:, mask].max()) if mask.any() else 0.0
-    lam, Q, rotated = jacobi_evd(G, tol, max_inner)
+    lam, Q, rotated = jacobi_evd(G, tol, max_inner, tol_mode)
     if bool(rotated.any()):
         sel = rotated
         Qs = Q[sel]

@@ -196,11 +196,11 @@ class DistributedBlockJacobi(Solver):
 
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
-                              metric, slot, mma=mma, pool=self._ws)
+                              metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode)
 
             def run_pair(a, b):
                 K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
-                               mma=mma, pool=self._ws)
+                               mma=mma, pool=self._ws, tol_mode=cfg.tol_mode)
 
             if not cfg.stagger:
                 run_pair = None
@@ -219,7 +219,8 @@ class DistributedBlockJacobi(Solver):
                         t_comm += time.perf_counter() - tc
                     with trace_range(f"svdj.round{r}"):
                         K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
-                                      cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws)
+                                      cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
+                                      tol_mode=cfg.tol_mode)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1

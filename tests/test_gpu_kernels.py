@@ -188,3 +188,62 @@ def test_bf16x6_matches_native(svdj, cuda, W):
     assert (a0 - a1).abs().max() / a0.abs().max() < 2e-6
     assert (v0 - v1).abs().max() < 2e-6
     assert orth[1] < 4 * orth[0] + 1e-6, orth
+
+
+@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64), (torch.float64, 32)])
+@pytest.mark.parametrize("full", [1, 0])
+def test_block_step_preconverged_pair_skipped(svdj, cuda, dtype, W, full):
+    """One pair already orthogonal (its EVD pass is skipped: D untouched in
+    cross mode, refreshed in full mode), one not: rotation count and D agree
+    with the torch reference (early exit vs rotation test)."""
+    K, R = svdj.ops.kernels, svdj.ops.reference
+    nb, m, m_pad = 4, 500, 512
+    n = nb * W
+    g = torch.Generator().manual_seed(4)
+    A64 = torch.zeros(n, m_pad, dtype=torch.float64)
+    # blocks 0 and 3: one orthogonal 2W-column panel (pair (0, 3) converged)
+    q, _ = torch.linalg.qr(torch.rand(m, 2 * W, generator=g, dtype=torch.float64))
+    q = q * torch.linspace(1, 4, 2 * W, dtype=torch.float64)
+    A64[0:W, :m] = q[:, :W].t()
+    A64[3 * W:4 * W, :m] = q[:, W:].t()
+    # blocks 1 and 2: each internally orthogonal, coupled to each other
+    for b in (1, 2):
+        qb, _ = torch.linalg.qr(torch.rand(m, W, generator=g, dtype=torch.float64))
+        A64[b * W:(b + 1) * W, :m] = (qb * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+    At = A64.to(dtype).to(cuda)
+    Vt = torch.zeros(n, 256, dtype=dtype, device=cuda)
+    K.set_identity(Vt, n)
+    D = K.col_norms2(At, m_pad)
+    D0 = D.double().cpu().clone()
+    pairs = torch.tensor([[[0, 3], [1, 2]]], dtype=torch.int32)
+    At64, Vt64, D64 = At.double().cpu(), Vt.double().cpu(), D.double().cpu()
+    tol = 1e-5 if dtype == torch.float32 else 1e-13
+    metric = K.new_metric(cuda)
+    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [full], tol, 1, metric)
+    _, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, bool(full), tol, 1)
+    _, nrot = K.read_metric(metric)
+    assert nrot == nrot_ref == 1
+    c03 = list(range(0, W)) + list(range(3 * W, 4 * W))
+    Dg = D.double().cpu()
+    rt = 1e-5 if dtype == torch.float32 else 1e-12
+    if not full:
+        assert torch.equal(Dg[c03], D0[c03])  # skipped pair: D untouched
+    torch.testing.assert_close(Dg[c03], D64[c03], rtol=rt, atol=0)
+    # the rotated pair's tracked norms equal its columns' (one EVD sweep leaves
+    # the eigenvalue order ordering-dependent, so compare with the data)
+    An = At.double().cpu()[W:3 * W, :m]
+    torch.testing.assert_close(Dg[W:3 * W], (An * An).sum(1), rtol=1e-4 if dtype == torch.float32
+                               else 1e-10, atol=1e-6)
+    # the skipped pair's columns of A and V are bit-identical to the input
+    assert torch.equal(At.double().cpu()[c03], A64.to(dtype).double()[c03])
+
+
+def test_block_absolute_threshold_stops(svdj, cuda):
+    """tol_mode='absolute' (the reference's |g_pq| > TOLERANCE rule) on the
+    block path: the sweeps stop once every |g_pq| is below tol."""
+    A = svdj.utils.inputs.random_dense(300, 256, dtype=torch.float64, seed=12)
+    res = svdj.svd(A.to(cuda), method="block", dtype=torch.float64, tol_mode="absolute",
+                   tol=1e-9, max_sweeps=40)
+    assert res.converged and res.sweeps < 40, res.history
+    rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["sigma_max_abs_err_over_smax"] < 1e-12, rep

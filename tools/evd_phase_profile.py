@@ -1,5 +1,10 @@
 """Per-phase cycle split of the block EVD kernel (dev aid; needs a library
-built with -DSVDJ_EVD_PROFILE, selected through SVDJ_HIP_LIB)."""
+built with -DSVDJ_EVD_PROFILE, selected through SVDJ_HIP_LIB).
+
+Slots (pair 0, wave 0 lane 0 and the last wave's lane 0): per step
+0 = block update (+ next-step solves in wave 0), 1 = Q rotation + DPP shift
+(Q waves), 2 = whole step incl. the barrier; per kernel 4 = setup (assembly,
+pre-pass, prologue), 5 = all sweeps."""
 import ctypes as C
 import json
 import os
@@ -14,19 +19,25 @@ K = svdj.ops.kernels
 fn = svdj.ops.hip_lib().svdj_debug_evd_profile
 fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 dev = torch.device("cuda:0")
-names = ["ph1_solve", "bar1_wait", "ph2_update", "bar2_wait", "dpp_shift"]
-for W in (32, 64):
-    n = 64 * W
-    At = torch.rand(n, n, device=dev)
-    Vt = torch.zeros(n, n, device=dev)
-    K.set_identity(Vt, n)
-    D = K.col_norms2(At, n)
-    pairs = torch.from_numpy(svdj.parallel.schedule.round_robin(n // W)).to(dev)
-    buf = (C.c_ulonglong * 16)()
-    fn(buf, 1)
-    K.block_steps(At, Vt, D, n, pairs[:8], W, [1] + [0] * 7, 1e-30, 1, K.new_metric(dev))
-    torch.cuda.synchronize()
-    fn(buf, 1)
-    steps = 8 * (2 * W - 1)
-    print(json.dumps({"W": W, "wave0_cycles_per_step": {k: round(buf[i] / steps, 1) for i, k in enumerate(names)},
-                      "lastwave_cycles_per_step": {k: round(buf[8 + i] / steps, 1) for i, k in enumerate(names)}}))
+names = {0: "update_solve", 1: "q_dpp", 2: "step_total", 4: "setup_per_kernel",
+         5: "sweeps_per_kernel"}
+for dt, Ws in ((torch.float32, (32, 64)), (torch.float64, (32,))):
+    for W in Ws:
+        n = 64 * W
+        At = torch.rand(n, n, device=dev, dtype=dt)
+        Vt = torch.zeros(n, n, device=dev, dtype=dt)
+        K.set_identity(Vt, n)
+        D = K.col_norms2(At, n)
+        pairs = torch.from_numpy(svdj.parallel.schedule.round_robin(n // W)).to(dev)
+        buf = (C.c_ulonglong * 16)()
+        K.block_steps(At, Vt, D, n, pairs[:8], W, [1] + [0] * 7, 1e-30, 1, K.new_metric(dev))
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        K.block_steps(At, Vt, D, n, pairs[8:16], W, [0] * 8, 1e-30, 1, K.new_metric(dev))
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        steps = 8 * (2 * W - 1)
+        out = {"dtype": str(dt), "W": W}
+        for who, off in (("wave0", 0), ("lastwave", 8)):
+            out[who] = {v: round(buf[off + k] / (steps if k < 4 else 8), 1) for k, v in names.items()}
+        print(json.dumps(out), flush=True)

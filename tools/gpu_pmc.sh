@@ -2,6 +2,8 @@
 # One pass per counter group (gfx950 slots: 8 SQ, 4 TCC, 2 GRBM per pass), each
 # its own run under a hard KILL timeout; a failing pass ends the script.
 # Usage: bash tools/gpu_pmc.sh OUTDIR N [extra bench args]
+#   PMC_CMD="python3 tools/evd_ab.py --n 4096" overrides the profiled program
+#   PMC_PASSES="1 2" selects passes (default: all)
 set -o pipefail
 export SVDJ_NO_AUTOBUILD=1
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -22,8 +24,10 @@ for want in "${PASSES[@]}"; do
   for c in $want; do  # keep the counters this box lists (a _sum suffix is derived)
     if grep -qw -- "${c%_sum}" $OUT/avail.txt; then ctr="$ctr $c"; else echo "skip $c"; fi
   done
+  if [ -n "$PMC_PASSES" ] && ! [[ " $PMC_PASSES " == *" $i "* ]]; then continue; fi
+  CMD=${PMC_CMD:-python3 $R/bench.py --n $N --steps 1 --warmup 0 --no-verify $EXTRA}
   timeout -s KILL 240 rocprofv3 --pmc $ctr -d $OUT/p$i -o run --output-format csv -- \
-    python3 $R/bench.py --n $N --steps 1 --warmup 0 --no-verify $EXTRA > $OUT/p$i.log 2>&1 \
+    $CMD > $OUT/p$i.log 2>&1 \
     || { echo "pass $i failed"; tail -20 $OUT/p$i.log; exit 1; }
   echo "pass $i ok: $ctr"
 done
