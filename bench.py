@@ -79,6 +79,26 @@ def verify_distributed(res, gen, m, n, comm, dtype):
             "orth_u_blockdiag_fro": float(parts[3].sqrt())}
 
 
+def verify_rows(res, gen, m, n, comm, dtype):
+    """QR-preconditioned (tall) result: U is this rank's row block, sigma and
+    V are complete on every rank.  ||A V - U S||_F / ||A||_F over all row
+    blocks, ||U^T U - I||_F (U^T U all-reduced) and ||V^T V - I||_F."""
+    r0, r1 = res.info["u_rows"]
+    A = torch.cat([gen(c0, min(c0 + 1024, n))[r0:r1] for c0 in range(0, n, 1024)], dim=1).to(dtype)
+    U, S, V = res.U.to(dtype), res.S.to(dtype), res.V.to(dtype)
+    eye = torch.eye(n, device=A.device, dtype=dtype)
+    UtU = U.t() @ U
+    parts = torch.stack([(A @ V - U * S).double().pow(2).sum(), A.double().pow(2).sum()])
+    if comm.distributed:
+        import torch.distributed as dist
+        dist.all_reduce(parts)
+        dist.all_reduce(UtU)
+    parts = parts.cpu()
+    return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
+            "orth_u_fro": float((UtU - eye).double().norm()),
+            "orth_v_fro": float((V.t() @ V - eye).double().norm())}
+
+
 def verify_root(res, A, dtype):
     """Rank 0, root-owned output: full ||A V - U S|| / ||A|| and orthogonality."""
     U, S, V = res.U.to(dtype), res.S.to(dtype), res.V.to(dtype)
@@ -108,14 +128,14 @@ def simulate(a, cfg, dtype, work):
     """Per-GPU time of rank g's plan in a P-GPU job, on one GPU."""
     import svdj
     from svdj.parallel import DistributedBlockJacobi, SimCommunicator
-    from svdj.utils.layout import pad_rows
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     P, g = a.simulate_P, a.simulate_rank
     n = a.n
     m = a.m or n
-    m_pad = pad_rows(m)
+    from svdj.models import precondition as pre
+    m_it = n if pre.use_qr(cfg, m, n) else m  # rows of the matrix the sweeps run on
     gen = make_generator(m, dev, work, dtype)
     seed_gen = torch.Generator(device=dev).manual_seed(99)
     made = []
@@ -123,8 +143,8 @@ def simulate(a, cfg, dtype, work):
     def seed(pos, like):  # other ranks' super-block halves: [A half, D half, V half]
         if pos == 0:
             t = torch.zeros_like(like)
-            t[:, :m] = torch.rand(like.shape[0], m, generator=seed_gen, device=dev,
-                                  dtype=work).to(like.dtype)
+            t[:, :m_it] = torch.rand(like.shape[0], m_it, generator=seed_gen, device=dev,
+                                     dtype=work).to(like.dtype)
             made.append(t)
             return t
         if pos == 1:  # squared norms of the matching A half
@@ -154,6 +174,7 @@ def simulate(a, cfg, dtype, work):
         "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
                    "chains": a.chains, "link_gbps_model": a.sim_link_gbps},
         "comm": res.info.get("comm"),
+        "qr_seconds": res.info.get("qr_seconds"),
         "sim_bytes_per_exchange": comm.bytes_moved // max(comm.exchanges, 1),
         "note": "exchanges swap with simulated peers (device copies of the real sizes); "
                 "numerics are not those of the real job -- timing only",
@@ -258,6 +279,8 @@ def main():
     if not a.no_verify:
         if a.root_owned:
             acc = verify_root(last, A_root, work) if comm.rank == 0 else None
+        elif last.info.get("precondition") == "qr":
+            acc = verify_rows(last, gen, m, n, comm, work)
         else:
             acc = verify_distributed(last, gen, m, n, comm, work)
     if comm.rank == 0:

@@ -63,6 +63,37 @@ def _cholqr2(A: torch.Tensor):
     return Q, R
 
 
+def dist_qr(A_loc: torch.Tensor, dtype: torch.dtype, comm):
+    """Row-distributed CholeskyQR2: rank g holds rows A_g (m_g x n) of A.
+
+    Twice: G = sum_g Q_g^T Q_g (local GEMM + one n x n all-reduce over
+    RCCL), G = L L^T (redundant on every rank: every rank sees the same G),
+    Q_g <- Q_g L^-T (local TRSM).  R = L2^T L1^T is replicated, so every rank
+    can take its super-blocks of R with no further communication, and Q stays
+    row-distributed (U = Q U_R is then a local GEMM per row block).  The QR
+    cost is divided by P; the replicated m x n factorisation it replaces
+    was redundant work on every rank.
+
+    Returns (Q_g, R), or None when the Gram is not numerically positive
+    definite (kappa(A) >~ eps^-1/2) -- the same decision on every rank."""
+    Q = A_loc.to(dtype)
+    eps = torch.finfo(dtype).eps
+    R = None
+    for it in range(2):
+        G = Q.t() @ Q
+        comm.allreduce_sum_(G)
+        L, info = torch.linalg.cholesky_ex(G)
+        if int(info) != 0 or not bool(torch.isfinite(L).all()):
+            return None
+        if it == 0:
+            d = torch.diagonal(L).abs()
+            if float(d.min()) <= eps ** 0.5 * float(d.max()):
+                return None
+        Q = torch.linalg.solve_triangular(L.t(), Q, upper=True, left=False)  # Q L^-T
+        R = L.t() if R is None else L.t() @ R
+    return Q, R
+
+
 def flops(m: int, n: int, sweeps: int, qr_used: bool) -> float:
     """Algorithmic work of a solve: the reference-form sweep count on the
     matrix actually iterated on, plus QR and the U GEMM when preconditioned."""

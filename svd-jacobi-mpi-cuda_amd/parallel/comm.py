@@ -142,6 +142,16 @@ class Communicator:
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        """(world, *t.shape) stack of every rank's ``t`` (RCCL all-gather)."""
+        flat = t.contiguous().reshape(-1)
+        out = torch.empty(self.world * flat.numel(), dtype=t.dtype, device=t.device)
+        if self.distributed:
+            dist.all_gather_into_tensor(out, flat)
+        else:
+            out.copy_(flat)
+        return out.view((self.world,) + tuple(t.shape))
+
     def barrier(self):
         if self.distributed:
             if self.backend == "nccl":
@@ -250,7 +260,18 @@ class SimCommunicator:
         return float(torch.as_tensor(mx).double()), float(torch.as_tensor(cnt).double())
 
     def allreduce_sum_(self, t):
+        """The sum over ``world`` ranks is modelled as ``world`` copies of this
+        rank's tensor.  For a square (Gram) tensor a small ridge keeps it as
+        well conditioned as the real all-reduced Gram of a tall matrix (one
+        row block alone can be square and ill-conditioned, which would push
+        the simulated CholeskyQR2 onto its Householder fallback): cost-only."""
+        t.mul_(self.world)
+        if t.dim() == 2 and t.shape[0] == t.shape[1]:
+            t.diagonal().add_(t.diagonal().mean() * 1e-2)
         return t
+
+    def allgather(self, t):
+        return torch.stack([t.clone() for _ in range(self.world)])
 
     def barrier(self):
         pass

@@ -74,10 +74,13 @@ class DistributedBlockJacobi(Solver):
               time_only: bool = False) -> SVDResult:
         """Distributed SVD.  ``dtype`` is the problem precision (fp32, fp64 or
         bf16 = bf16 data on fp32 master copies and bf16 matrix cores).  Tall
-        inputs (m >= qr_ratio n, or precondition="qr") are QR-preconditioned:
-        every rank factors the generated A redundantly (no communication), or
-        rank 0 factors its root-owned A; the sweeps then run on R (n x n) and
-        U = Q U_R (models/precondition.py)."""
+        inputs (m >= qr_ratio n, or precondition="qr") are QR-preconditioned
+        with a row-distributed CholeskyQR2 (``precondition.dist_qr``: local
+        Gram, RCCL all-reduce, replicated Cholesky, local TRSM); the sweeps
+        then run on the replicated R (n x n) and U = Q U_R is a local GEMM
+        per row block.  That path returns U as this rank's row block
+        (``info["u_rows"]``) with sigma and V complete on every rank, or U
+        complete on rank 0 with ``gather``."""
         comm, cfg = self.comm, self.config
         dev = comm.device
         jobu, jobv = SVDOptions.parse(jobu), SVDOptions.parse(jobv)
@@ -100,37 +103,119 @@ class DistributedBlockJacobi(Solver):
             res = self._solve(A, jobu, jobv, m, n, dtype, generator, gather, time_only)
             res.info["flops"] = pre.flops(m, n, res.sweeps, False)
             return res
-        # ---- QR-preconditioned tall-skinny solve
-        Q = None
+        # ---- QR-preconditioned tall-skinny solve, row-distributed: rank g
+        # owns rows [r0, r1) of A and of U; R (n x n) is replicated
+        P, g = comm.world, comm.rank
+        r0, r1 = g * m // P, (g + 1) * m // P
+        t_qr = time.perf_counter()
         if generator is not None:
-            Afull = torch.cat([generator(c0, min(c0 + 1024, n)) for c0 in range(0, n, 1024)],
-                              dim=1).to(device=dev, dtype=work)
-            Q, R = pre.qr(Afull, work)
-            del Afull
-            res = self._solve(None, jobu, jobv, n, n, dtype, lambda c0, c1: R[:, c0:c1], gather,
-                              time_only)
+            A_loc = torch.cat([generator(c0, min(c0 + 1024, n))[r0:r1].to(device=dev, dtype=work)
+                               for c0 in range(0, n, 1024)], dim=1)
         else:
-            R = None
-            if comm.rank == 0:
-                Q, R = pre.qr(A.to(dev), work)
-            res = self._solve(R, jobu, jobv, n, n, dtype, None, gather, time_only)
-            if comm.distributed and jobu != SVDOptions.NoVec and res.info.get("distributed_output"):
-                if Q is None:
-                    Q = torch.empty(m, n, dtype=work, device=dev)
-                comm.broadcast(Q, 0)
-        if jobu != SVDOptions.NoVec and res.U is not None and Q is not None:
-            if res.info.get("distributed_output"):
-                Ut = res.U  # (2B, pad(n)) transposed local columns of U_R
-                Uloc = Q @ Ut[:, :n].to(work).t()
-                At = torch.zeros(Ut.shape[0], pad_rows(m), dtype=Ut.dtype, device=dev)
-                At[:, :m] = Uloc.t()
-                res.U = At
-                res.info["geometry"] = {**res.info["geometry"], "m_pad": pad_rows(m)}
-            else:
-                res.U = (Q @ res.U.to(work)).to(res.U.dtype)
-        res.info["precondition"] = "qr"
-        res.info["flops"] = pre.flops(m, n, res.sweeps, True)
+            A_loc = self._scatter_rows(A, m, n, work)
+        out = pre.dist_qr(A_loc, work, comm)
+        if out is None:  # too ill-conditioned for CholeskyQR2: replicated Householder
+            Qf, R = pre.qr(self._allgather_rows(A_loc, m, n), work, method="householder")
+            Q_loc = Qf[r0:r1].contiguous()
+            del Qf
+        else:
+            Q_loc, R = out
+        del A_loc
+        if cfg.comm_timing and dev.type == "cuda":  # phase timing costs a sync
+            torch.cuda.synchronize(dev)
+        t_qr = time.perf_counter() - t_qr
+        res = self._solve(None, jobu, jobv, n, n, dtype, lambda c0, c1: R[:, c0:c1], False,
+                          time_only)
+        want_u = jobu != SVDOptions.NoVec
+        U_R, S, V = self._allgather_columns(res, n, want_u, jobv != SVDOptions.NoVec)
+        U_loc = (Q_loc @ U_R).to(U_R.dtype) if want_u else None
+        res.S, res.V = S, V
+        res.info.update(precondition="qr", flops=pre.flops(m, n, res.sweeps, True),
+                        qr_seconds=round(t_qr, 4),
+                        distributed_output="rows" if P > 1 and not gather else False,
+                        u_rows=(r0, r1))
+        if gather and P > 1 and want_u:
+            U_loc = self._gather_rows(U_loc, m, n)
+        res.U = U_loc
+        if dtype == torch.bfloat16 and (gather or P == 1):
+            res.U = res.U.to(torch.bfloat16) if res.U is not None else None
+            res.V = res.V.to(torch.bfloat16) if res.V is not None else None
         return res
+
+    # -------------------------------------------------- row-distributed QR I/O
+    def _row_range(self, h: int, m: int):
+        P = self.comm.world
+        return h * m // P, (h + 1) * m // P
+
+    def _scatter_rows(self, A, m, n, dtype):
+        """Root-owned A: rank 0 sends every rank its row block (one grouped batch)."""
+        comm = self.comm
+        r0, r1 = self._row_range(comm.rank, m)
+        if not comm.distributed:
+            return A.to(device=comm.device, dtype=dtype)
+        if comm.rank == 0:
+            Ad = A.to(device=comm.device, dtype=dtype)
+            sends = [(Ad[self._row_range(h, m)[0]:self._row_range(h, m)[1]].contiguous(), h)
+                     for h in range(1, comm.world)]
+            comm.sendrecv(sends, [])
+            return Ad[r0:r1].contiguous()
+        out = torch.empty(r1 - r0, n, dtype=dtype, device=comm.device)
+        comm.sendrecv([], [(out, 0)])
+        return out
+
+    def _allgather_rows(self, A_loc, m, n):
+        """Every rank's row block, assembled on every rank (Householder fallback)."""
+        comm = self.comm
+        if not comm.distributed:
+            return A_loc
+        rows = max(self._row_range(h, m)[1] - self._row_range(h, m)[0] for h in range(comm.world))
+        buf = torch.zeros(rows, n, dtype=A_loc.dtype, device=A_loc.device)
+        buf[:A_loc.shape[0]] = A_loc
+        allr = comm.allgather(buf)
+        return torch.cat([allr[h, :self._row_range(h, m)[1] - self._row_range(h, m)[0]]
+                          for h in range(comm.world)])
+
+    def _gather_rows(self, U_loc, m, n):
+        """Row blocks of U to rank 0 (one grouped batch); None on other ranks."""
+        comm = self.comm
+        if comm.rank != 0:
+            comm.sendrecv([(U_loc.contiguous(), 0)], [])
+            return None
+        parts = [U_loc]
+        recvs = []
+        for h in range(1, comm.world):
+            a, b = self._row_range(h, m)
+            t = torch.empty(b - a, n, dtype=U_loc.dtype, device=U_loc.device)
+            parts.append(t)
+            recvs.append((t, h))
+        comm.sendrecv([], recvs)
+        return torch.cat(parts)
+
+    def _allgather_columns(self, res, n, want_u, want_v):
+        """All of U_R (n x n), sigma (n) and V (n x n) on every rank, from each
+        rank's resident super-block columns (transposed layout)."""
+        comm = self.comm
+        geo = res.info["geometry"]
+        B = geo["B"]
+        held = torch.tensor(res.info["held"], dtype=torch.int64, device=res.S.device)
+        ids = comm.allgather(held).cpu()
+        S_all = comm.allgather(res.S)
+        U_all = comm.allgather(res.U) if want_u else None
+        V_all = comm.allgather(res.V) if want_v else None
+        ncols = 2 * B * comm.world
+        S = torch.zeros(ncols, dtype=res.S.dtype, device=res.S.device)
+        Ut = torch.zeros(ncols, n, dtype=res.S.dtype, device=res.S.device) if want_u else None
+        Vt = torch.zeros(ncols, n, dtype=res.S.dtype, device=res.S.device) if want_v else None
+        for h in range(comm.world):
+            for s_ in range(2):
+                sb = int(ids[h, s_])
+                dst, src = slice(sb * B, (sb + 1) * B), slice(s_ * B, (s_ + 1) * B)
+                S[dst] = S_all[h, src]
+                if want_u:
+                    Ut[dst] = U_all[h, src, :n]
+                if want_v:
+                    Vt[dst] = V_all[h, src, :n]
+        return (Ut[:n].t() if want_u else None), S[:n], (Vt[:n].t() if want_v else None)
 
     def _solve(self, A, jobu, jobv, m, n, pdtype, generator, gather, time_only) -> SVDResult:
         comm, cfg = self.comm, self.config

@@ -15,7 +15,7 @@ def main():
     mode = sys.argv[5] if len(sys.argv) > 5 else "root"
     comm = Communicator(backend="gloo", device=torch.device("cpu"))
     cfg = svdj.SolverConfig(block=W, dtype=torch.float64, max_inner_sweeps=1,
-                            precondition="qr" if mode.endswith("qr") else "none")
+                            precondition="qr" if "qr" in mode else "none")
     solver = DistributedBlockJacobi(cfg, comm)
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=9)
     if mode == "roundtrip":  # reference test_local_matrix_distribution_* parity
@@ -48,6 +48,28 @@ def main():
             rep.update(sweeps=res.sweeps, converged=res.converged, world=comm.world)
             with open(out, "w") as f:
                 json.dump(rep, f)
+        comm.destroy()
+        return
+    if mode == "genqr_rows":  # row-distributed QR output: U row block, full S and V
+        import torch.distributed as dist
+        res = solver.solve(None, m=m, n=n, dtype=torch.float64,
+                           generator=lambda c0, c1: A[:, c0:c1], gather=False)
+        r0, r1 = res.info["u_rows"]
+        U, S, V = res.U, res.S, res.V
+        parts = torch.stack([(A[r0:r1] @ V - U * S).pow(2).sum(), A[r0:r1].pow(2).sum()])
+        UtU = U.t() @ U
+        dist.all_reduce(parts)
+        dist.all_reduce(UtU)
+        if comm.rank == 0:
+            eye = torch.eye(n, dtype=torch.float64)
+            ref = torch.linalg.svdvals(A)
+            with open(out, "w") as f:
+                json.dump({"residual_rel": float((parts[0] / parts[1]).sqrt()),
+                           "orth_u_fro": float((UtU - eye).norm()),
+                           "orth_v_fro": float((V.t() @ V - eye).norm()),
+                           "sigma_err": float((torch.sort(S, descending=True).values - ref).abs().max()
+                                              / ref[0]),
+                           "rows": [r0, r1], "converged": res.converged, "world": comm.world}, f)
         comm.destroy()
         return
     if mode in ("root", "rootqr"):

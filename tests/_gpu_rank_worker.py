@@ -6,7 +6,7 @@ or gloo, host-synchronised).  Solves one fixed matrix with the pipelined
 distributed solver and writes rank 0's gathered (U, S, V) plus run info to
 the output file, so runs over different backends can be compared bitwise.
 
-argv: n W chains mode(otf|root) out.pt
+argv: n W chains mode(otf|root|qr) out.pt
 """
 import json
 import os
@@ -28,11 +28,14 @@ def main():
                             precondition="none")
     solver = DistributedBlockJacobi(cfg, comm)
     g = torch.Generator(device=dev).manual_seed(5)
-    A = torch.rand(n, n, generator=g, device=dev, dtype=torch.float32)
+    m = 4 * n if mode == "qr" else n
+    if mode == "qr":  # tall: row-distributed CholeskyQR2 + Jacobi on R
+        cfg.precondition = "qr"
+    A = torch.rand(m, n, generator=g, device=dev, dtype=torch.float32)
     if mode == "root":
         res = solver.solve(A if comm.rank == 0 else None, gather=True)
     else:
-        res = solver.solve(None, m=n, n=n, dtype=torch.float32,
+        res = solver.solve(None, m=m, n=n, dtype=torch.float32,
                            generator=lambda c0, c1: A[:, c0:c1], gather=True)
     if comm.rank == 0:
         torch.save({"U": res.U.cpu(), "S": res.S.cpu(), "V": res.V.cpu(), "A": A.cpu(),

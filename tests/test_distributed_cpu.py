@@ -94,3 +94,14 @@ def test_simulated_rank_plan_cpu():
     geo = res.info["geometry"]
     half = geo["B"] // 2
     assert comm.bytes_moved == comm.exchanges * half * 8 * (geo["m_pad"] + 1 + geo["n_v"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_row_distributed_cholqr2(world, tmp_path):
+    """Tall-skinny: row-distributed CholeskyQR2 (local Gram + all-reduce,
+    replicated Cholesky, local TRSM), Jacobi on the replicated R, U = Q U_R
+    per row block; checked globally (all-reduced) on every rank's rows."""
+    rep = _run(world, 400, 96, 32, tmp_path, mode="genqr_rows")
+    assert rep["converged"] and rep["world"] == world
+    assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-10, rep
+    assert rep["orth_v_fro"] < 1e-10 and rep["sigma_err"] < 1e-12, rep

@@ -50,6 +50,7 @@ def _check_accuracy(d):
     assert d["converged"], d["history"]
     assert float((A @ V - U * S).norm() / A.norm()) < 2e-5
     assert float((V.t() @ V - eye).norm()) < 2e-3
+    assert float((U.t() @ U - eye).norm()) < 5e-2
     ref = torch.linalg.svdvals(A)
     got = torch.sort(S, descending=True).values
     assert float((got - ref).abs().max() / ref[0]) < 2e-6
@@ -74,4 +75,12 @@ def test_rccl_root_owned_scatter_gather(tmp_path):
 
 def test_rccl_single_chain_blocking_exchange(tmp_path):
     r = _run(2, "nccl", tmp_path / "c1.pt", n=512, chains=1)
+    _check_accuracy(r)
+
+
+def test_rccl_row_distributed_qr(tmp_path):
+    """Tall 2048 x 512 over 2 RCCL ranks: row-distributed CholeskyQR2 (Gram
+    all-reduce), Jacobi on R, U = Q U_R per row block, gathered to rank 0."""
+    r = _run(2, "nccl", tmp_path / "qr.pt", n=512, mode="qr")
+    assert r["U"].shape == (2048, 512)
     _check_accuracy(r)
