@@ -36,21 +36,41 @@ constexpr int kApplyThreads = 256;
 __host__ __device__ constexpr int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------- gram
-template <typename T, int W, bool FULL>
+// MODE: GRAM_CROSS  C = A_bi^T A_bj (W x W slab per pair and row chunk);
+//       GRAM_FULL   G = [A_bi A_bj]^T [..] (2W x 2W slab), one launch;
+//       GRAM_SPLIT  the same 2W x 2W slab in three regions (A_bi^T A_bi,
+//                   A_bj^T A_bj, A_bi^T A_bj), one per blockIdx.z: the
+//                   one-launch form keeps 2W(2W+1)/2 tile accumulators, which
+//                   for fp64 W = 64 exceed the register file.
+// For fp64 W = 64 the cross products are also split over blockIdx.z in XS = 2
+// row halves (x tiles), so accumulators plus the double-buffered loads fit in
+// registers without spilling.
+enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2 };
+template <typename T, int W>
+__host__ __device__ constexpr int gram_xsplit() { return (sizeof(T) == 8 && W == 64) ? 2 : 1; }
+
+template <typename T, int W, int MODE>
 __global__ __launch_bounds__(kGramThreads) void gram_kernel(
     const T* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
     int rows_per_chunk, T* __restrict__ slabs) {
   using M = Mfma<T>;
+  constexpr bool FULL = MODE == GRAM_FULL;
   constexpr int TL = M::TILE;
-  constexpr int HT = W / TL;      // column tiles per block
-  constexpr int NCT = 2 * HT;     // column tiles in X
-  constexpr int NTP = FULL ? NCT * (NCT + 1) / 2 : HT * HT;
+  constexpr int HT = W / TL;                             // column tiles per block
+  constexpr int XS = FULL ? 1 : gram_xsplit<T, W>();     // row halves over blockIdx.z
+  constexpr int HTX = HT / XS;                           // x tiles of this workgroup
+  constexpr int NCT = FULL ? 2 * HT : HTX + HT;          // column tiles loaded
+  constexpr int NTP = FULL ? NCT * (NCT + 1) / 2 : HTX * HT;
   constexpr int LPL = M::LPL;
-  constexpr int SLAB = FULL ? 4 * W * W : W * W;
+  constexpr int SLAB = FULL ? 4 * W * W : HTX * TL * W;  // this workgroup's reduction
   constexpr int WAVES = kGramThreads / SVDJ_WAVE;
+  static_assert(HT % XS == 0, "x tiles split evenly");
 
   const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
-  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int region = MODE == GRAM_SPLIT ? (int)blockIdx.z / XS : 2;
+  const int xpart = FULL ? 0 : (int)blockIdx.z % XS;
+  const int pi = pairs[2 * pair], pj = pairs[2 * pair + 1];
+  const int bi = region == 1 ? pj : pi, bj = region == 0 ? pi : pj;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r_begin = chunk * rows_per_chunk;
   const int r_end = min(m_pad, r_begin + rows_per_chunk);
@@ -63,8 +83,15 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   const T* colp[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
-    const int blk = ct < HT ? bi : bj;
-    const int col = blk * W + (ct % HT) * TL + M::lane_col(lane);
+    int blk, tile;
+    if constexpr (FULL) {
+      blk = ct < HT ? bi : bj;
+      tile = ct % HT;
+    } else {
+      blk = ct < HTX ? bi : bj;
+      tile = ct < HTX ? xpart * HTX + ct : ct - HTX;
+    }
+    const int col = blk * W + tile * TL + M::lane_col(lane);
     colp[ct] = A + (size_t)col * lda + M::lane_kg(lane) * LPL;
   }
 
@@ -97,10 +124,10 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
           }
       } else {
 #pragma unroll
-        for (int a = 0; a < HT; ++a)
+        for (int a = 0; a < HTX; ++a)
 #pragma unroll
           for (int b = 0; b < HT; ++b) {
-            acc[idx] = M::mfma(v[a][t], v[HT + b][t], acc[idx]);
+            acc[idx] = M::mfma(v[a][t], v[HTX + b][t], acc[idx]);
             ++idx;
           }
       }
@@ -137,7 +164,7 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
           }
       } else {
 #pragma unroll
-        for (int a = 0; a < HT; ++a)
+        for (int a = 0; a < HTX; ++a)
 #pragma unroll
           for (int b = 0; b < HT; ++b) {
 #pragma unroll
@@ -152,8 +179,27 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
     }
     __syncthreads();
   }
-  T* out = slabs + ((size_t)pair * nchunk + chunk) * SLAB;
-  for (int i = threadIdx.x; i < SLAB; i += kGramThreads) out[i] = red[i];
+  const int xoff = xpart * HTX * TL;  // first row of this workgroup's part
+  if constexpr (MODE == GRAM_SPLIT) {  // this region's quadrant(s) of the 2W x 2W slab
+    constexpr int N = 2 * W;
+    T* out = slabs + ((size_t)pair * nchunk + chunk) * 4 * W * W;
+    for (int i = threadIdx.x; i < SLAB; i += kGramThreads) {
+      const int a = xoff + i / W, b = i % W;
+      const T v = red[i];
+      if (region == 0) out[a * N + b] = v;
+      if (region == 1) out[(W + a) * N + W + b] = v;
+      if (region == 2) {
+        out[a * N + W + b] = v;
+        out[(W + b) * N + a] = v;
+      }
+    }
+  } else if constexpr (FULL) {
+    T* out = slabs + ((size_t)pair * nchunk + chunk) * SLAB;
+    for (int i = threadIdx.x; i < SLAB; i += kGramThreads) out[i] = red[i];
+  } else {
+    T* out = slabs + ((size_t)pair * nchunk + chunk) * (W * W) + xoff * W;
+    for (int i = threadIdx.x; i < SLAB; i += kGramThreads) out[i] = red[i];
+  }
 }
 
 // -------------------------------------------------------------------- evd
@@ -1138,12 +1184,18 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
   const int full = c.modes ? c.modes[s] : 0;
-  if (full)
-    hipLaunchKernelGGL((gram_kernel<T, W, true>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
-                       c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
-  else
-    hipLaunchKernelGGL((gram_kernel<T, W, false>), dim3(c.P, c.g.gchunks), dim3(kGramThreads), 0,
-                       c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  constexpr int XS = gram_xsplit<T, W>();
+  if (full) {
+    if constexpr (XS > 1)  // see GRAM_SPLIT
+      hipLaunchKernelGGL((gram_kernel<T, W, GRAM_SPLIT>), dim3(c.P, c.g.gchunks, 3 * XS),
+                         dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+    else
+      hipLaunchKernelGGL((gram_kernel<T, W, GRAM_FULL>), dim3(c.P, c.g.gchunks),
+                         dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  } else {
+    hipLaunchKernelGGL((gram_kernel<T, W, GRAM_CROSS>), dim3(c.P, c.g.gchunks, XS),
+                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  }
   SVDJ_LAUNCH_CHECK();
   hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
                      c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode, max_inner,
@@ -1350,8 +1402,9 @@ static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int
   if (dtype == 0 && W == 32) return steps_dispatch<float, 32>(SVDJ_STEPS_ARGS);
   if (dtype == 0 && W == 64) return steps_dispatch<float, 64>(SVDJ_STEPS_ARGS);
   if (dtype == 1 && W == 32) return steps_dispatch<double, 32>(SVDJ_STEPS_ARGS);
+  if (dtype == 1 && W == 64) return steps_dispatch<double, 64>(SVDJ_STEPS_ARGS);
 #undef SVDJ_STEPS_ARGS
-  set_error("unsupported (dtype=%d, W=%d); supported: fp32 W in {32,64}, fp64 W=32", dtype, W);
+  set_error("unsupported (dtype=%d, W=%d); supported: W in {32, 64}", dtype, W);
   return -3;
 }
 
@@ -1471,6 +1524,10 @@ extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
   else if (dtype == 1 && mma == 0 && W == 32)
     hipLaunchKernelGGL((apply_kernel<double, 32>), grid, blk, 0, st, (double*)X, ld, chunks,
+                       rows_chunk, rows, (double*)nullptr, 0, 0, 0, dbuf, (const double*)Q,
+                       dbuf + 2);
+  else if (dtype == 1 && mma == 0 && W == 64)
+    hipLaunchKernelGGL((apply_kernel<double, 64>), grid, blk, 0, st, (double*)X, ld, chunks,
                        rows_chunk, rows, (double*)nullptr, 0, 0, 0, dbuf, (const double*)Q,
                        dbuf + 2);
   else {

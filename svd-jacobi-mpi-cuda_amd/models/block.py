@@ -18,7 +18,10 @@ from .base import SVDResult, Solver, Timer
 
 def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     if dtype == torch.float64:
-        return 32
+        # fp64: the apply is MFMA-bound from W=32 on, W=64 halves the steps.
+        # Measured (MI355X, s per solve W=32 / W=64): 8192: 2.50 / 2.92,
+        # 16384: 17.8 / 16.5 (profiles/r2_configs).
+        return 64 if n >= 12288 else 32
     # fp32: W=64 halves the per-byte traffic of the Gram and needs half the
     # steps, but its EVD is 4.5x slower (280 vs 62 us).  Measured with the
     # staggered chains (MI355X, n x n, s per solve W=32 / W=64): 2048: 0.087 /

@@ -21,7 +21,7 @@ from . import reference as ref
 from ._native import NativeError, hip_check, hip_lib
 
 ROW_ALIGN = 128
-SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32,)}
+SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32, 64)}
 # Matrix-core modes of the block apply (csrc/hip/block.hip): native f32/f64
 # MFMA (default, fp32-exact products and sums), or fp32 data on bf16 MFMA
 # with a 3-way / 2-way operand split -- faster (memory-bound instead of

@@ -59,8 +59,8 @@ def test_scalar_step_matches_reference(svdj, cuda, dtype):
 
 
 @pytest.mark.parametrize("dtype,W,mma", [(torch.float32, 32, "native"), (torch.float32, 64, "native"),
-                                         (torch.float64, 32, "native"), (torch.float32, 32, "bf16x6"),
-                                         (torch.float32, 64, "bf16x6")])
+                                         (torch.float64, 32, "native"), (torch.float64, 64, "native"),
+                                         (torch.float32, 32, "bf16x6"), (torch.float32, 64, "bf16x6")])
 @pytest.mark.parametrize("full", [1, 0])
 def test_block_step_matches_reference(svdj, cuda, dtype, W, mma, full):
     """One gram -> evd -> apply step vs the fp64 torch reference on the same input."""
@@ -190,7 +190,8 @@ def test_bf16x6_matches_native(svdj, cuda, W):
     assert orth[1] < 4 * orth[0] + 1e-6, orth
 
 
-@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64), (torch.float64, 32)])
+@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64), (torch.float64, 32),
+                                     (torch.float64, 64)])
 @pytest.mark.parametrize("full", [1, 0])
 def test_block_step_preconverged_pair_skipped(svdj, cuda, dtype, W, full):
     """One pair already orthogonal (its EVD pass is skipped: D untouched in
@@ -247,3 +248,16 @@ def test_block_absolute_threshold_stops(svdj, cuda):
     assert res.converged and res.sweeps < 40, res.history
     rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
     assert rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
+
+
+@pytest.mark.parametrize("W", [32, 64])
+def test_fp64_block_widths_end_to_end(svdj, cuda, W):
+    """fp64 at both block widths (fp64 W=64: split full Gram, 137 KB LDS EVD,
+    147 KB LDS apply) converges to fp64 accuracy against LAPACK's sigma."""
+    m, n = 700, 512
+    A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=21)
+    res = svdj.svd(A.to(cuda), method="block", dtype=torch.float64, block=W)
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 5e-12 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
+    assert rep["orth_u_fro"] < 5e-11 and rep["orth_v_fro"] < 5e-11, rep

@@ -19,3 +19,7 @@ run fp64_10000 400 --n 10000 --dtype fp64 --steps 1 --warmup 0
 run fp64_16384 600 --n 16384 --dtype fp64 --steps 1 --warmup 0 --no-verify
 run fp64_20000 900 --n 20000 --dtype fp64 --steps 1 --warmup 0 --no-verify --progress
 run fp64_30000 1100 --n 30000 --dtype fp64 --steps 1 --warmup 0 --no-verify --progress
+# BASELINE config 5 (65536^2 fp32) feasibility: two sweeps on one GPU, and one
+# full-work sweep of rank 0's plan in the 8-GPU job
+run big65536_2sweeps 900 --n 65536 --dtype fp32 --steps 1 --warmup 0 --no-verify --max-sweeps 2 --progress
+run sim_big65536_p8 900 --n 65536 --dtype fp32 --simulate-P 8 --sim-sweeps 1
