@@ -198,6 +198,8 @@ def main():
     p.add_argument("--block", type=int, default=None)
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
+    p.add_argument("--tol", type=float, default=None,
+                   help="rotation threshold (default 4 sqrt(m) eps of the problem dtype)")
     p.add_argument("--chains", type=int, default=2)
     p.add_argument("--no-stagger", action="store_true",
                    help="issue the two step chains independently (lockstep) instead of offset")
@@ -224,7 +226,7 @@ def main():
 
     dtype = {"fp32": torch.float32, "fp64": torch.float64, "bf16": torch.bfloat16}[a.dtype]
     work = torch.float64 if dtype == torch.float64 else torch.float32
-    cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps,
+    cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps, tol=a.tol,
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
                             stagger=not a.no_stagger, precondition=a.precondition,
                             progress=a.progress, comm_timing=a.gpus > 1)
