@@ -199,7 +199,7 @@ def main():
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--inner", type=int, default=1)
     p.add_argument("--tol", type=float, default=None,
-                   help="rotation threshold (default 4 sqrt(m) eps of the problem dtype)")
+                   help="rotation threshold (default sqrt(m) eps of the problem dtype)")
     p.add_argument("--chains", type=int, default=2)
     p.add_argument("--no-stagger", action="store_true",
                    help="issue the two step chains independently (lockstep) instead of offset")

@@ -46,7 +46,7 @@ class SolverConfig:
     method: str = "auto"            # auto | block | scalar | oracle
     dtype: torch.dtype | None = None  # fp32 | fp64 | bf16 (None: the input's dtype)
     block: int | None = None        # block width W (block path); None: auto
-    tol: float | None = None        # rotation threshold; None: 4 sqrt(m) eps
+    tol: float | None = None        # rotation threshold; None: sqrt(m) eps (utils.metrics.default_tol)
     tol_mode: str = "relative"      # relative | absolute (reference parity)
     max_sweeps: int = 60            # reference: 1 (main.cu:482)
     max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)

@@ -58,7 +58,8 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
   hipStream_t st;
   CHECK(hipStreamCreate(&st));
   std::vector<double> hist(max_sweeps, 0.0);
-  if (tol <= 0) tol = 4.0 * std::sqrt((double)m) * (sizeof(T) == 8 ? 2.220446049250313e-16 : 1.1920929e-07);
+  // sqrt(m) eps (LAPACK xGESVJ), as utils/metrics.py default_tol
+  if (tol <= 0) tol = std::sqrt((double)m) * (sizeof(T) == 8 ? 2.220446049250313e-16 : 1.1920929e-07);
 
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));

@@ -183,5 +183,5 @@ def finalize(At, scale_u=True):
 
 
 def default_tol(dtype, m):
-    eps = torch.finfo(dtype).eps
-    return 4.0 * math.sqrt(max(m, 1)) * eps
+    from ..utils.metrics import default_tol as _dt
+    return _dt(dtype, m)

@@ -61,11 +61,15 @@ def verify(A, U, S, V, sigma_ref=None) -> dict:
 
 
 def default_tol(dtype: torch.dtype, m: int) -> float:
-    """Relative rotation threshold: 4 sqrt(m) eps (computed dot products of
-    length m carry ~sqrt(m) eps relative noise; tighter never stops).  For
-    bf16 problems eps = 2^-21: above the 2-way bf16 split's product noise
-    (~8 fp32 ulps per apply, tools/probe_apply.py), far below the bf16 output
-    rounding, and tight enough that the last sweeps converge quadratically
-    (a 2^-17 level left the final phase crawling along the threshold)."""
-    eps = 2.0 ** -21 if dtype == torch.bfloat16 else torch.finfo(dtype).eps
-    return 4.0 * math.sqrt(max(m, 1)) * eps
+    """Relative rotation threshold.  fp32 / fp64: sqrt(m) eps, the LAPACK
+    xGESVJ value (computed dot products of length m carry ~sqrt(m) eps
+    relative noise).  Round 1 needed 4 sqrt(m) eps while the split-K Gram
+    slabs were summed in the data precision; with fp64 slab sums the tighter
+    value converges at +1-2 % time and halves ||U^T U - I|| per factor of 2
+    (16384^2 fp32: 0.40 -> 0.098, profiles/r2_tol).  bf16 problems: 4 sqrt(m)
+    2^-21 -- above the 2-way bf16 split's product noise (~8 fp32 ulps per
+    apply, tools/probe_apply.py), far below the bf16 output rounding, and
+    tight enough that the last sweeps converge quadratically."""
+    if dtype == torch.bfloat16:
+        return 4.0 * math.sqrt(max(m, 1)) * 2.0 ** -21
+    return math.sqrt(max(m, 1)) * torch.finfo(dtype).eps
