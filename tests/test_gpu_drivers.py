@@ -47,8 +47,9 @@ def test_distributed_world1_gpu_matches_svdvals(svdj, cuda):
     A = svdj.utils.inputs.random_dense(700, 512, dtype=torch.float64, seed=4).to(cuda)
     res = DistributedBlockJacobi(svdj.SolverConfig(dtype=torch.float32, block=32), comm).solve(A)
     rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A.cpu()))
-    assert res.converged and rep["sigma_max_abs_err_over_smax"] < 1e-5, rep
-    assert rep["orth_v_fro"] < 5e-3, rep
+    # measured ~1.4e-7 / ~5e-5 / ~4e-4 at this size (tools/measure_test_accuracy.py)
+    assert res.converged and rep["sigma_max_abs_err_over_smax"] < 1e-6, rep
+    assert rep["orth_v_fro"] < 3e-4 and rep["orth_u_fro"] < 2e-3, rep
 
 
 def test_block_solver_deterministic(svdj, cuda):

@@ -115,6 +115,17 @@ def test_block_step_matches_reference(svdj, cuda, dtype, W, mma, full):
                                rtol=0, atol=vtol)
 
 
+# (residual, sigma, ||U^TU-I||, ||V^TV-I||) bounds ~5x the values measured on
+# MI355X with the default sqrt(m) eps threshold (tools/measure_test_accuracy.py)
+_E2E_BOUNDS = {
+    ("block", torch.float32, "native"): (8e-6, 1e-6, 1.5e-3, 2e-4),
+    ("block", torch.float32, "bf16x6"): (8e-6, 1e-6, 1.5e-3, 2e-4),
+    ("block", torch.float64, "native"): (2e-12, 1e-12, 2e-12, 1.5e-11),
+    ("scalar", torch.float32, "native"): (2e-4, 4e-5, 1.5e-3, 8e-3),
+    ("scalar", torch.float64, "native"): (5e-13, 3e-13, 2e-12, 8e-12),
+}
+
+
 @pytest.mark.parametrize("method,dtype,mma", [("block", torch.float32, "native"),
                                               ("block", torch.float32, "bf16x6"),
                                               ("block", torch.float64, "native"),
@@ -126,11 +137,9 @@ def test_svd_end_to_end(svdj, cuda, method, dtype, mma):
     res = svdj.svd(A.to(cuda), method=method, dtype=dtype, mma=mma)
     assert res.converged, res.history
     rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
-    eps = torch.finfo(dtype).eps
-    assert rep["residual_rel"] < 2000 * eps, rep
-    assert rep["sigma_max_abs_err_over_smax"] < 2000 * eps, rep
-    assert rep["orth_u_fro"] < 50 * math.sqrt(n) * 4 * math.sqrt(m) * eps * 10, rep
-    assert rep["orth_v_fro"] < 2e4 * math.sqrt(n) * eps, rep
+    r, sg, ou, ov = _E2E_BOUNDS[(method, dtype, mma)]
+    assert rep["residual_rel"] < r and rep["sigma_max_abs_err_over_smax"] < sg, rep
+    assert rep["orth_u_fro"] < ou and rep["orth_v_fro"] < ov, rep
 
 
 def test_gesvd_inplace_reference_signature(svdj, cuda):
