@@ -56,17 +56,26 @@ def _run(cmd, verbose):
     return r
 
 
-def build_cpu(force: bool = False, verbose: bool = False) -> Path:
-    LIBDIR.mkdir(exist_ok=True)
-    if not force and not _stale(CPU_LIB, CPU_SOURCES + HEADERS + [Path(__file__)]):
-        return CPU_LIB
+ASAN_CPU_LIB = LIBDIR / "asan" / "libsvdj_cpu.so"
+
+
+def build_cpu(force: bool = False, verbose: bool = False, asan: bool = False) -> Path:
+    """Host library.  ``asan``: AddressSanitizer + UBSan build into lib/asan/
+    (host code only -- GPU sanitizers are not available); load it with
+    SVDJ_CPU_LIB=<path> and the interpreter started under
+    LD_PRELOAD=$(gcc -print-file-name=libasan.so) (tools/asan_cpu_tests.sh)."""
+    target = ASAN_CPU_LIB if asan else CPU_LIB
+    target.parent.mkdir(parents=True, exist_ok=True)
+    if not force and not _stale(target, CPU_SOURCES + HEADERS + [Path(__file__)]):
+        return target
     cxx = os.environ.get("CXX", "g++")
-    tmp = CPU_LIB.with_suffix(".so.tmp")
-    cmd = [cxx, "-O3", "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-Wall",
+    tmp = target.with_suffix(".so.tmp")
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1", "-g"] if asan else ["-O3"]
+    cmd = [cxx, *san, "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-Wall",
            f"-I{CSRC / 'include'}", *CPU_SOURCES, "-o", tmp]
     _run(cmd, verbose)
-    os.replace(tmp, CPU_LIB)
-    return CPU_LIB
+    os.replace(tmp, target)
+    return target
 
 
 def build_hip(force: bool = False, verbose: bool = False, jobs: int = 4) -> Path:

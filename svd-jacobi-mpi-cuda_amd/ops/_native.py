@@ -60,7 +60,8 @@ def cpu_lib():
     with _lock:
         if _cpu is not None:
             return _cpu
-        lib = C.CDLL(str(_ensure_built("cpu")))
+        override = os.environ.get("SVDJ_CPU_LIB")  # e.g. the host-ASan build
+        lib = C.CDLL(override if override else str(_ensure_built("cpu")))
         _sig(lib, "svdj_sameh_num_steps", c_int, [c_int])
         _sig(lib, "svdj_sameh_schedule", c_int, [c_int, c_i32_p])
         _sig(lib, "svdj_round_robin", c_int, [c_int, c_i32_p])
