@@ -99,6 +99,31 @@ def verify_rows(res, gen, m, n, comm, dtype):
             "orth_v_fro": float((V.t() @ V - eye).double().norm())}
 
 
+def sigma_check(res, gen, m, n, comm):
+    """max |sigma - sigma_ref| / sigma_ref_max against an fp64 oracle
+    (torch.linalg.svdvals of the regenerated A in fp64 on the device,
+    rocSOLVER), after the timed region.  Every rank's sigma columns are
+    all-gathered first (padding columns dropped)."""
+    if res.info.get("distributed_output") is True:
+        B = res.info["geometry"]["B"]
+        ids = comm.allgather(torch.tensor(res.info["held"], device=res.S.device)).cpu()
+        S_all = comm.allgather(res.S)
+        sig = torch.zeros(2 * B * comm.world, dtype=torch.float64, device=res.S.device)
+        for h in range(comm.world):
+            for s_ in range(2):
+                sb = int(ids[h, s_])
+                sig[sb * B:(sb + 1) * B] = S_all[h, s_ * B:(s_ + 1) * B].double()
+        sig = sig[:n]
+    else:
+        sig = res.S.double()
+    if comm.rank != 0:
+        return None
+    A = gen(0, n).double()
+    ref = torch.linalg.svdvals(A)
+    got = torch.sort(sig, descending=True).values
+    return float((got - ref).abs().max() / ref[0])
+
+
 def verify_root(res, A, dtype):
     """Rank 0, root-owned output: full ||A V - U S|| / ||A|| and orthogonality."""
     U, S, V = res.U.to(dtype), res.S.to(dtype), res.V.to(dtype)
@@ -219,6 +244,8 @@ def main():
     p.add_argument("--json-out", default=None)
     p.add_argument("--no-verify", action="store_true",
                    help="skip the post-timing accuracy check")
+    p.add_argument("--check-sigma", action="store_true",
+                   help="also compare sigma with an fp64 oracle (svdvals), after timing")
     a = p.parse_args()
 
     import svdj
@@ -285,6 +312,10 @@ def main():
             acc = verify_rows(last, gen, m, n, comm, work)
         else:
             acc = verify_distributed(last, gen, m, n, comm, work)
+    if a.check_sigma and last.info.get("precondition") != "qr":
+        err = sigma_check(last, gen, m, n, comm)
+        if comm.rank == 0:
+            acc = dict(acc or {}, sigma_max_rel_err_vs_fp64_oracle=err)
     if comm.rank == 0:
         line = {
             "metric": BASELINE_METRIC,
