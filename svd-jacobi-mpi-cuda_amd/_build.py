@@ -134,9 +134,37 @@ def build_driver(force: bool = False, verbose: bool = False) -> Path:
     return DRIVER_BIN
 
 
+DIST_SRC = CSRC / "dist" / "svdj_dist.cpp"
+DIST_LIB = LIBDIR / "libsvdj_dist.so"
+DIST_DRIVER_SRC = CSRC / "driver" / "svdj_dist_main.cpp"
+DIST_DRIVER_BIN = PKG / "bin" / "svdj_dist_main"
+
+
+def build_dist(force: bool = False, verbose: bool = False) -> Path:
+    """Native distributed solver (svdj_dist.h: RCCL tournament over the HIP
+    block kernels) and its fork launcher ``bin/svdj_dist_main``."""
+    cpu, hip = build_cpu(force, verbose), build_hip(force, verbose)
+    deps = [DIST_SRC, cpu, hip, Path(__file__)] + HEADERS
+    if force or _stale(DIST_LIB, deps):
+        tmp = DIST_LIB.with_suffix(".so.tmp")
+        _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}",
+              f"-I{CSRC / 'include'}", DIST_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_hip",
+              "-lsvdj_cpu", "-lrccl", "-Wl,-rpath,$ORIGIN"], verbose)
+        os.replace(tmp, DIST_LIB)
+    DIST_DRIVER_BIN.parent.mkdir(exist_ok=True)
+    if force or _stale(DIST_DRIVER_BIN, [DIST_DRIVER_SRC, DIST_LIB] + deps):
+        tmp = DIST_DRIVER_BIN.with_suffix(".tmp")
+        _run([_hipcc(), "-O2", "-std=c++17", "-Wall", f"--offload-arch={ARCH}",
+              f"-I{CSRC / 'include'}", DIST_DRIVER_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_dist",
+              "-lsvdj_hip", "-lsvdj_cpu", "-lrccl", "-Wl,-rpath,$ORIGIN/../lib"], verbose)
+        os.replace(tmp, DIST_DRIVER_BIN)
+    return DIST_DRIVER_BIN
+
+
 def build_all(force: bool = False, verbose: bool = False) -> dict:
     return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose)),
-            "driver": str(build_driver(force, verbose))}
+            "driver": str(build_driver(force, verbose)),
+            "dist": str(build_dist(force, verbose))}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,409 @@
+// Native multi-GPU driver: the reference's MPI binary (`mpirun -np P
+// SVD_Jacobi_MPI_CUDA <n>`, reference main.cu:1426-1676 and
+// build/runSVDMPICUDAWithoutCMake.slurm) rebuilt on RCCL, one process per GPU,
+// with no Python and no MPI.
+//
+//   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
+//                  [--dtype f32|f64] [--block W] [--max-sweeps K] [--tol T]
+//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--no-v]
+//                  [--shared-gpu] [--verify] [--timeout SEC] [--id-file PATH]
+//
+// The launcher forks P ranks before anything touches the GPU (the parent never
+// does) and waits for them; a rank that fails or a job that exceeds --timeout
+// ends every rank.  Launched by an external one-process-per-GPU launcher
+// instead (RANK / WORLD_SIZE / LOCAL_RANK in the environment, no --np), the
+// process runs its own rank only and the ranks meet through --id-file (or
+// SVDJ_DIST_ID), which must name a path all ranks see.
+//
+// Rank g selects GPU LOCAL_RANK (or g); --shared-gpu puts every rank on GPU 0
+// and gives each its own NCCL_HOSTID so RCCL accepts several ranks on one
+// device (transport: sockets on loopback, for rehearsal on a one-GPU box).
+// Every rank generates the reference input (svdj_ref_*_input) and keeps the
+// columns of the two super-blocks the tournament starts it with; rank 0
+// prints the reference's lines and, with --verify, gathers U, S, V and checks
+// ||A - U S V^T||_F and orthogonality in fp64 on the host.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "svdj_cpu.h"
+#include "svdj_dist.h"
+#include "svdj_hip.h"
+
+namespace {
+
+struct Opts {
+  int n = 0, m = 0, np = 0, W = 32, max_sweeps = 60, mma = 0;
+  unsigned seed = 1000000;
+  double tol = -1, timeout = 600;
+  bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;
+  std::string id_file;
+};
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      std::fprintf(stderr, "[rank %d] HIP error %s at %s:%d\n", rank, hipGetErrorString(e_), \
+                   __FILE__, __LINE__);                                                    \
+      return 2;                                                                            \
+    }                                                                                      \
+  } while (0)
+#define NK(x)                                                                                \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess) {                                                                 \
+      std::fprintf(stderr, "[rank %d] RCCL error %s at %s:%d\n", rank, ncclGetErrorString(r_), \
+                   __FILE__, __LINE__);                                                      \
+      return 2;                                                                              \
+    }                                                                                        \
+  } while (0)
+
+template <typename T>
+int run_rank(const Opts& o, int rank, int world, int device) {
+  const int dtype = sizeof(T) == 8 ? 1 : 0;
+  const ncclDataType_t nt = dtype ? ncclFloat64 : ncclFloat32;
+  CK(hipSetDevice(device));
+  void* comm = nullptr;
+  if (svdj_dist_comm_init(rank, world, o.id_file.c_str(), o.timeout, &comm) < 0) {
+    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
+    return 2;
+  }
+  ncclComm_t nc = (ncclComm_t)comm;
+  const int m = o.m, n = o.n;
+  int B, ncols, m_pad, n_v;
+  if (svdj_dist_geometry(world, m, n, o.W, &B, &ncols, &m_pad, &n_v) < 0) {
+    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
+    return 1;
+  }
+  int32_t held[2];
+  svdj_dist_initial_held(world, rank, held);
+
+  // reference input (every rank draws the same stream), keep this rank's columns
+  std::vector<double> A((size_t)m * n, 0.0);
+  if (o.dense)
+    svdj_ref_dense_input(m, n, A.data(), m, o.seed);
+  else
+    svdj_ref_triu_input(m, n, A.data(), m, o.seed);
+  std::vector<T> hA((size_t)2 * B * m_pad, T(0));
+  for (int s = 0; s < 2; ++s)
+    for (int c = 0; c < B; ++c) {
+      const int j = held[s] * B + c;
+      if (j >= n) break;
+      for (int i = 0; i < m; ++i) hA[(size_t)(s * B + c) * m_pad + i] = (T)A[(size_t)j * m + i];
+    }
+  if (rank != 0 || !o.verify) std::vector<double>().swap(A);
+
+  hipStream_t sa, sb;
+  CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  T *dA, *dV = nullptr, *dD, *dS;
+  double* dt;
+  CK(hipMalloc((void**)&dA, hA.size() * sizeof(T)));
+  if (o.want_v) CK(hipMalloc((void**)&dV, (size_t)2 * B * n_v * sizeof(T)));
+  CK(hipMalloc((void**)&dD, (size_t)2 * B * sizeof(T)));
+  CK(hipMalloc((void**)&dS, (size_t)2 * B * sizeof(T)));
+  CK(hipMalloc((void**)&dt, sizeof(double)));
+  CK(hipMemcpy(dA, hA.data(), hA.size() * sizeof(T), hipMemcpyHostToDevice));
+  double tol = o.tol;
+  if (tol <= 0)  // sqrt(m) eps (LAPACK xGESVJ), as utils/metrics.py default_tol
+    tol = std::sqrt((double)m) * (dtype ? 2.220446049250313e-16 : 1.1920929e-07);
+
+  // ---- timed region: V = I, column norms, sweeps, sigma / U normalisation
+  NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclSum, nc, sa));  // barrier
+  CK(hipStreamSynchronize(sa));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int s = 0; s < 2 && o.want_v; ++s)
+    if (svdj_set_identity(dtype, dV + (size_t)s * B * n_v, n_v, n_v, B, held[s] * B, sa) < 0) {
+      std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
+      return 2;
+    }
+  if (svdj_col_norms2(dtype, dA, m_pad, m_pad, 2 * B, dD, sa) < 0) {
+    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
+    return 2;
+  }
+  std::vector<double> hist(o.max_sweeps, 0.0);
+  svdj_dist_problem p{};
+  p.rank = rank;
+  p.world = world;
+  p.comm = comm;
+  p.dtype = dtype;
+  p.W = o.W;
+  p.m_pad = m_pad;
+  p.n_v = n_v;
+  p.B = B;
+  p.At = dA;
+  p.Vt = dV;
+  p.D = dD;
+  p.held[0] = held[0];
+  p.held[1] = held[1];
+  p.tol = tol;
+  p.tol_mode = o.abs_tol ? 1 : 0;
+  p.max_sweeps = o.max_sweeps;
+  p.mma = o.mma;
+  p.stream_a = sa;
+  p.stream_b = sb;
+  p.hist = hist.data();
+  if (svdj_dist_solve(&p, dS) < 0) {
+    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
+    return 2;
+  }
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  CK(hipMemcpy(dt, &secs, sizeof(double), hipMemcpyHostToDevice));
+  NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, nc, sa));
+  CK(hipMemcpyAsync(&secs, dt, sizeof(double), hipMemcpyDeviceToHost, sa));
+  CK(hipStreamSynchronize(sa));
+
+  if (rank == 0) {
+    std::printf("%s\n", svdj_hip_version());
+    std::printf("Dimensions, height: %d, width: %d\n", m, n);
+    std::printf("ranks: %d  block W: %d  super-block B: %d  %s\n", world, o.W, B,
+                o.shared ? "(shared GPU)" : "");
+    std::printf("SVD MPI+OMP time with U,V calculation: %.6f\n", secs);
+    std::printf("sweeps: %d  converged: %d  last off value: %.3e  tol: %.3e\n", p.sweeps,
+                p.converged, p.sweeps > 0 ? hist[p.sweeps - 1] : 0.0, tol);
+    const double flops = (double)n * (n - 1) / 2.0 * (12.0 * m + (o.want_v ? 6.0 * n : 0.0)) * p.sweeps;
+    std::printf("GFLOP/s (algorithmic): %.1f\n", flops / secs / 1e9);
+  }
+
+  int rc = 0;
+  if (o.verify) {
+    // gather (held, sigma, U columns, V columns) on rank 0
+    int32_t* dh;
+    CK(hipMalloc((void**)&dh, 2 * world * sizeof(int32_t)));
+    CK(hipMemcpy(dh + 2 * rank, p.held, 2 * sizeof(int32_t), hipMemcpyHostToDevice));
+    T *gA = nullptr, *gV = nullptr, *gS = nullptr;
+    if (rank == 0) {
+      CK(hipMalloc((void**)&gA, (size_t)world * 2 * B * m_pad * sizeof(T)));
+      CK(hipMalloc((void**)&gS, (size_t)world * 2 * B * sizeof(T)));
+      if (o.want_v) CK(hipMalloc((void**)&gV, (size_t)world * 2 * B * n_v * sizeof(T)));
+    }
+    NK(ncclGroupStart());
+    if (rank == 0) {
+      for (int r = 1; r < world; ++r) {
+        NK(ncclRecv(dh + 2 * r, 2, ncclInt32, r, nc, sa));
+        NK(ncclRecv(gA + (size_t)r * 2 * B * m_pad, (size_t)2 * B * m_pad, nt, r, nc, sa));
+        NK(ncclRecv(gS + (size_t)r * 2 * B, (size_t)2 * B, nt, r, nc, sa));
+        if (o.want_v) NK(ncclRecv(gV + (size_t)r * 2 * B * n_v, (size_t)2 * B * n_v, nt, r, nc, sa));
+      }
+    } else {
+      NK(ncclSend(dh + 2 * rank, 2, ncclInt32, 0, nc, sa));
+      NK(ncclSend(dA, (size_t)2 * B * m_pad, nt, 0, nc, sa));
+      NK(ncclSend(dS, (size_t)2 * B, nt, 0, nc, sa));
+      if (o.want_v) NK(ncclSend(dV, (size_t)2 * B * n_v, nt, 0, nc, sa));
+    }
+    NK(ncclGroupEnd());
+    CK(hipStreamSynchronize(sa));
+    if (rank == 0) {
+      CK(hipMemcpy(gA, dA, (size_t)2 * B * m_pad * sizeof(T), hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(gS, dS, (size_t)2 * B * sizeof(T), hipMemcpyDeviceToDevice));
+      if (o.want_v) CK(hipMemcpy(gV, dV, (size_t)2 * B * n_v * sizeof(T), hipMemcpyDeviceToDevice));
+      std::vector<int32_t> hh(2 * world);
+      std::vector<T> hU((size_t)world * 2 * B * m_pad), hS((size_t)world * 2 * B),
+          hV(o.want_v ? (size_t)world * 2 * B * n_v : 0);
+      CK(hipMemcpy(hh.data(), dh, hh.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hU.data(), gA, hU.size() * sizeof(T), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hS.data(), gS, hS.size() * sizeof(T), hipMemcpyDeviceToHost));
+      if (o.want_v) CK(hipMemcpy(hV.data(), gV, hV.size() * sizeof(T), hipMemcpyDeviceToHost));
+      // local slot (r, s) holds global columns [hh[2r+s] B, +B)
+      std::vector<double> U((size_t)n * m), S(n), V(o.want_v ? (size_t)n * n : 0);
+      std::vector<int> seen(2 * world, 0);
+      for (int r = 0; r < world; ++r)
+        for (int s = 0; s < 2; ++s) {
+          const int sb = hh[2 * r + s];
+          if (sb < 0 || sb >= 2 * world || seen[sb]++) {
+            std::fprintf(stderr, "bad final placement: super-block %d\n", sb);
+            rc = 4;
+          }
+          for (int c = 0; c < B && rc == 0; ++c) {
+            const int j = sb * B + c;
+            if (j >= n) break;
+            const size_t src = (size_t)(r * 2 + s) * B + c;
+            S[j] = hS[src];
+            for (int i = 0; i < m; ++i) U[(size_t)j * m + i] = hU[src * m_pad + i];
+            if (o.want_v)
+              for (int i = 0; i < n; ++i) V[(size_t)j * n + i] = hV[src * n_v + i];
+          }
+        }
+      if (rc == 0) {
+        double anorm = 0;
+        for (double x : A) anorm += x * x;
+        anorm = std::sqrt(anorm);
+        const double ou = svdj_cpu_orth_f64(m, n, U.data(), m, 0);
+        std::printf("||U^TU-I||_F: %.3e\n", ou);
+        if (o.want_v) {
+          const double resid = svdj_cpu_residual_f64(m, n, n, A.data(), m, U.data(), m, S.data(),
+                                                     V.data(), n, 0);
+          const double ov = svdj_cpu_orth_f64(n, n, V.data(), n, 0);
+          std::printf("||A-USVt||_F: %.6e\n||A-USVt||_F/||A||_F: %.3e\n||V^TV-I||_F: %.3e\n", resid,
+                      resid / anorm, ov);
+          const double lim = dtype ? 1e-10 : 1e-4;
+          if (!(resid / anorm < lim)) {
+            std::fprintf(stderr, "verification failed: relative residual %.3e >= %.1e\n",
+                         resid / anorm, lim);
+            rc = 5;
+          }
+        }
+      }
+      (void)hipFree(gA);
+      (void)hipFree(gS);
+      (void)hipFree(gV);
+    }
+    (void)hipFree(dh);
+  }
+  if (rank == 0 && !p.converged) std::printf("warning: not converged in %d sweeps\n", p.sweeps);
+  (void)hipFree(dA);
+  (void)hipFree(dV);
+  (void)hipFree(dD);
+  (void)hipFree(dS);
+  (void)hipFree(dt);
+  svdj_dist_comm_destroy(comm);
+  return rc;
+}
+
+int rank_main(const Opts& o, int rank, int world, int local) {
+  if (o.shared) {
+    const std::string host = "svdj-shared-gpu-rank" + std::to_string(rank);
+    setenv("NCCL_HOSTID", host.c_str(), 1);
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    setenv("NCCL_IB_DISABLE", "1", 0);
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    std::fprintf(stderr, "[rank %d] no GPU\n", rank);
+    return 2;
+  }
+  const int device = o.shared ? 0 : local % ndev;
+  if (!o.shared && world > ndev) {
+    std::fprintf(stderr, "%d ranks but %d GPUs (use --shared-gpu to rehearse on one)\n", world, ndev);
+    return 1;
+  }
+  return o.f32 ? run_rank<float>(o, rank, world, device) : run_rank<double>(o, rank, world, device);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s N --np P [--m M] [--dtype f32|f64] [--block W] [--shared-gpu] [--verify] ...\n",
+                 argv[0]);
+    return 1;
+  }
+  Opts o;
+  o.n = std::atoi(argv[1]);
+  std::string mma = "native";
+  for (int i = 2; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+    if (a == "--m") o.m = std::atoi(next());
+    else if (a == "--np") o.np = std::atoi(next());
+    else if (a == "--input") o.dense = std::string(next()) == "dense";
+    else if (a == "--seed") o.seed = (unsigned)std::strtoul(next(), nullptr, 10);
+    else if (a == "--dtype") o.f32 = std::string(next()) == "f32";
+    else if (a == "--block") o.W = std::atoi(next());
+    else if (a == "--max-sweeps") o.max_sweeps = std::atoi(next());
+    else if (a == "--tol") o.tol = std::atof(next());
+    else if (a == "--abs-tol") o.abs_tol = true;
+    else if (a == "--mma") mma = next();
+    else if (a == "--no-v") o.want_v = false;
+    else if (a == "--shared-gpu") o.shared = true;
+    else if (a == "--verify") o.verify = true;
+    else if (a == "--timeout") o.timeout = std::atof(next());
+    else if (a == "--id-file") o.id_file = next();
+    else {
+      std::fprintf(stderr, "unknown option %s\n", a.c_str());
+      return 1;
+    }
+  }
+  if (o.m == 0) o.m = o.n;
+  if (o.n < 1 || o.m < o.n) {
+    std::fprintf(stderr, "N >= 1 and m >= N required\n");
+    return 1;
+  }
+  if (o.f32) o.mma = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
+
+  const char* env_rank = std::getenv("RANK");
+  const char* env_world = std::getenv("WORLD_SIZE");
+  if (o.np == 0 && env_rank && env_world) {  // external launcher: this process is one rank
+    if (o.id_file.empty()) {
+      const char* e = std::getenv("SVDJ_DIST_ID");
+      const char* port = std::getenv("MASTER_PORT");
+      o.id_file = e ? e : std::string("/tmp/svdj_dist_") + (port ? port : "0") + ".id";
+    }
+    const char* lr = std::getenv("LOCAL_RANK");
+    const int rank = std::atoi(env_rank);
+    const int rc = rank_main(o, rank, std::atoi(env_world), lr ? std::atoi(lr) : rank);
+    if (rank == 0) std::remove(o.id_file.c_str());
+    return rc;
+  }
+  if (o.np < 1) o.np = 1;
+  if (o.id_file.empty()) o.id_file = "/tmp/svdj_dist_" + std::to_string(getpid()) + ".id";
+  std::remove(o.id_file.c_str());
+  std::fflush(stdout);
+  // fork every rank before anything touches the GPU; the parent only waits
+  std::vector<pid_t> pids;
+  for (int r = 0; r < o.np; ++r) {
+    const pid_t pid = fork();
+    if (pid < 0) {
+      std::perror("fork");
+      for (pid_t q : pids) kill(q, SIGKILL);
+      return 2;
+    }
+    if (pid == 0) {
+      const int rc = rank_main(o, r, o.np, r);
+      std::fflush(stdout);
+      std::fflush(stderr);
+      _exit(rc);
+    }
+    pids.push_back(pid);
+  }
+  int worst = 0, alive = o.np;
+  std::vector<char> done(o.np, 0);
+  auto stop_others = [&](int sig) {  // only children not yet reaped (their pids are ours)
+    for (int r = 0; r < o.np; ++r)
+      if (!done[r]) kill(pids[r], sig);
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  while (alive > 0) {
+    int st = 0;
+    const pid_t pid = waitpid(-1, &st, WNOHANG);
+    if (pid > 0) {
+      --alive;
+      int who = -1;
+      for (int r = 0; r < o.np; ++r)
+        if (pids[r] == pid) who = r;
+      if (who >= 0) done[who] = 1;
+      const int code = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
+      if (code != 0) {
+        std::fprintf(stderr, "rank %d exited with %d; stopping the job\n", who, code);
+        if (!worst) {
+          worst = code;
+          stop_others(SIGTERM);
+        }
+      }
+      continue;
+    }
+    if (pid < 0) break;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > o.timeout + 30) {
+      std::fprintf(stderr, "job exceeded %.0f s; stopping the ranks\n", o.timeout);
+      stop_others(SIGKILL);
+      worst = 124;
+      o.timeout = 1e30;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  std::remove(o.id_file.c_str());
+  return worst;
+}
