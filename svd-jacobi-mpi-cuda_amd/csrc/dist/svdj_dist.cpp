@@ -1,20 +1,19 @@
 // Native distributed block one-sided Jacobi (svdj_dist.h): RCCL + the HIP
-// block kernels of libsvdj_hip, no Python.
+// block kernels of libsvdj_hip, no Python.  Same plan as the Python executor
+// (parallel/pipeline.py, parallel/distributed.py):
 //
 // Per sweep on GPU g (slots 0 and 1 hold super-blocks of k = B/W blocks,
-// each split in halves 0|1 of k/2 blocks):
-//   round 0: round robin inside each slot        (chain a: slot 0, b: slot 1)
-//   every round r: cross pairs between the slots as four half tasks
-//       phase 1: I0 x S0 (a) || I1 x S1 (b)
-//       phase 2: I0 x S1 (a) || I1 x S0 (b)      (I = incoming slot, S = other)
-//   between rounds: the slot named by the tournament is sent to one peer and
-//   replaced by the block received from another (one grouped
-//   ncclSend/ncclRecv, reference scatter/gather main.cu:582-680, 854-936).
-// Each phase is one svdj_block_steps2 call (chain b's step s starts when
-// chain a's EVD of step s is done); the two streams meet at phase ends.  The
-// stop test is an RCCL all-reduce (max of the float-ordered uint32
-// convergence value, sum of rotated pairs) per sweep: the value the
-// reference computes and discards (main.cu:710).
+// each split in halves 0|1 of k/2 blocks; I = incoming slot, S = the other):
+//   round 0 : round robin inside each slot            (chain 0: slot 0, 1: slot 1)
+//   round r : I0xS0 (0), I0xS1 (0), I1xS0 (1), send half 0 of the slot
+//             replaced next, I1xS1 (1), send half 1   (last round: no sends)
+// Tasks on different chains touching disjoint halves are issued as one
+// staggered svdj_block_steps2 pair; every dependency (half -> task, task ->
+// send, arrival -> consumer) is a HIP event, so exchanges overlap the compute
+// of the other halves (reference main.cu:582-680, 854-936 sends whole blocks
+// with blocking MPI between rounds).  The stop test is an RCCL all-reduce (max
+// of the float-ordered uint32 convergence value, sum of rotated pairs) per
+// sweep: the value the reference computes and discards (main.cu:710).
 #include "svdj_dist.h"
 
 #include <hip/hip_runtime.h>
@@ -88,12 +87,12 @@ struct Task {
 };
 
 int upload(Task& t, const std::vector<int32_t>& host, int steps, int npairs,
-           std::vector<int32_t> modes, hipStream_t st) {
+           std::vector<int32_t> modes) {
   t.steps = steps;
   t.npairs = npairs;
   t.modes = std::move(modes);
   HIPC(hipMalloc((void**)&t.pairs, host.size() * sizeof(int32_t)));
-  HIPC(hipMemcpyAsync(t.pairs, host.data(), host.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  HIPC(hipMemcpy(t.pairs, host.data(), host.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -149,6 +148,11 @@ extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* n
   return 0;
 }
 
+extern "C" int svdj_dist_choose_block(int dtype, int world, int n) {
+  (void)dtype;  // same crossover for fp32 and fp64 (models/block.py measurements)
+  return n / (world > 0 ? world : 1) >= 12288 ? 64 : 32;
+}
+
 extern "C" int svdj_dist_initial_held(int world, int rank, int32_t held[2]) {
   Tour t(world);
   held[0] = t.h(0, rank, 0);
@@ -156,13 +160,127 @@ extern "C" int svdj_dist_initial_held(int world, int rank, int32_t held[2]) {
   return 0;
 }
 
+namespace {
+
+// ---- sweep plan of one GPU (parallel/pipeline.py sweep_plan / issue_groups)
+// Halves are keyed slot*2 + half.  Tasks carry their device pairs and the
+// stream (chain) they run on; a Send moves one half of one slot.
+struct Item {
+  bool send = false;
+  const Task* task = nullptr;
+  int stream = 0, hv[2] = {0, 0};  // task: chain and the two halves it touches
+  int round = 0, slot = 0, half = 0;  // send
+};
+
+std::vector<Item> sweep_items(const Tour& t, int g, const Task rr[2], const Task cross[2][2][2]) {
+  std::vector<Item> it;
+  auto task = [&](const Task* tk, int stream, int h0, int h1) {
+    Item x;
+    x.task = tk;
+    x.stream = stream;
+    x.hv[0] = h0;
+    x.hv[1] = h1;
+    it.push_back(x);
+  };
+  auto send = [&](int r, int slot, int half) {
+    Item x;
+    x.send = true;
+    x.round = r;
+    x.slot = slot;
+    x.half = half;
+    it.push_back(x);
+  };
+  task(&rr[0], 0, 0, 1);
+  task(&rr[1], 1, 2, 3);
+  for (int r = 0; r < t.R; ++r) {
+    const int inc = r ? t.x(r, g) : 0, stay = 1 - inc;
+    auto T = [&](int ih, int sh, int stream) {
+      task(&cross[inc][ih][sh], stream, inc * 2 + ih, stay * 2 + sh);
+    };
+    if (r + 1 == t.R) {  // nothing to send: two fully parallel phases
+      T(0, 0, 0), T(1, 1, 1), T(0, 1, 0), T(1, 0, 1);
+      continue;
+    }
+    const int nxt = t.x(r + 1, g);
+    T(0, 0, 0), T(0, 1, 0), T(1, 0, 1);
+    send(r + 1, nxt, 0);
+    T(1, 1, 1);
+    send(r + 1, nxt, 1);
+  }
+  return it;
+}
+
+// Issue order: a task is paired with the next task (at most one Send in
+// between) when they run on different chains, touch disjoint halves and the
+// Send concerns neither half of the second; the Send is issued after the pair.
+struct Group {
+  int a = -1, b = -1;  // item indices (b = -1: single task; a is a Send if items[a].send)
+};
+
+std::vector<Group> issue_groups(const std::vector<Item>& it) {
+  std::vector<Group> out;
+  const int n = (int)it.size();
+  int i = 0;
+  while (i < n) {
+    if (!it[i].send) {
+      int j = i + 1;
+      while (j < n && it[j].send) ++j;
+      if (j < n && j - i - 1 <= 1) {
+        const Item &x = it[i], &y = it[j];
+        bool ok = y.stream != x.stream;
+        for (int u : x.hv)
+          for (int v : y.hv) ok = ok && u != v;
+        for (int s = i + 1; s < j; ++s)
+          for (int v : y.hv) ok = ok && it[s].slot * 2 + it[s].half != v;
+        if (ok) {
+          out.push_back({i, j});
+          for (int s = i + 1; s < j; ++s) out.push_back({s, -1});
+          i = j + 1;
+          continue;
+        }
+      }
+    }
+    out.push_back({i, -1});
+    ++i;
+  }
+  return out;
+}
+
+}  // namespace
+
+extern "C" int svdj_dist_plan(int world, int rank, int32_t* out, int cap) {
+  if (world < 1 || rank < 0 || rank >= world) return fail(-2, "bad plan args");
+  Tour tour(world);
+  Task rr[2], cross[2][2][2];
+  const std::vector<Item> items = sweep_items(tour, rank, rr, cross);
+  const std::vector<Group> groups = issue_groups(items);
+  if ((int)groups.size() > cap) return fail(-2, "plan has %zu groups, cap %d", groups.size(), cap);
+  for (size_t i = 0; i < groups.size(); ++i) {
+    int32_t* o = out + 7 * i;
+    const Item& a = items[groups[i].a];
+    for (int j = 0; j < 7; ++j) o[j] = -1;
+    if (a.send) {
+      o[0] = 2, o[1] = a.round, o[2] = a.slot, o[3] = a.half;
+      continue;
+    }
+    o[0] = groups[i].b < 0 ? 0 : 1;
+    o[1] = a.stream, o[2] = a.hv[0], o[3] = a.hv[1];
+    if (groups[i].b >= 0) {
+      const Item& b = items[groups[i].b];
+      o[4] = b.stream, o[5] = b.hv[0], o[6] = b.hv[1];
+    }
+  }
+  return (int)groups.size();
+}
+
 extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   const int P = p->world, g = p->rank, W = p->W, B = p->B;
-  const int k = B / W, hk = k / 2;
+  const int k = B / W, hk = k / 2, hB = hk * W;
   if (B % W || k < 2 || k % 2) return fail(-2, "B=%d must hold an even number of W=%d blocks", B, W);
   if (p->stream_a == p->stream_b) return fail(-2, "two distinct streams needed");
   const size_t es = p->dtype == 1 ? 8 : 4;
-  hipStream_t sa = (hipStream_t)p->stream_a, sb = (hipStream_t)p->stream_b;
+  hipStream_t st[2] = {(hipStream_t)p->stream_a, (hipStream_t)p->stream_b};
+  hipStream_t sa = st[0];
   ncclComm_t comm = (ncclComm_t)p->comm;
   const ncclDataType_t nt = p->dtype == 1 ? ncclFloat64 : ncclFloat32;
   Tour tour(P);
@@ -173,14 +291,15 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   Task rr_task[2], cross[2][2][2];  // cross[incoming slot][I half][S half]
   std::vector<int32_t> rr_modes(k - 1, 0);
   rr_modes[0] = 1;  // the first step of a sweep re-measures the diagonal (full Gram)
-  for (int s = 0; s < 2; ++s) {
+  int rc = 0;
+  for (int s = 0; s < 2 && !rc; ++s) {
     std::vector<int32_t> h = rr;
     for (auto& v : h) v += s * k;
-    if (int rc = upload(rr_task[s], h, k - 1, k / 2, rr_modes, sa)) return rc;
+    rc = upload(rr_task[s], h, k - 1, k / 2, rr_modes);
   }
   for (int inc = 0; inc < 2; ++inc)
     for (int ih = 0; ih < 2; ++ih)
-      for (int sh = 0; sh < 2; ++sh) {
+      for (int sh = 0; sh < 2 && !rc; ++sh) {
         const int stay = 1 - inc;
         std::vector<int32_t> h((size_t)hk * hk * 2);
         for (int t = 0; t < hk; ++t)
@@ -188,36 +307,37 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
             h[(t * hk + a) * 2] = inc * k + ih * hk + a;
             h[(t * hk + a) * 2 + 1] = stay * k + sh * hk + (a + t) % hk;
           }
-        if (int rc = upload(cross[inc][ih][sh], h, hk, hk, std::vector<int32_t>(hk, 0), sa)) return rc;
+        rc = upload(cross[inc][ih][sh], h, hk, hk, std::vector<int32_t>(hk, 0));
       }
+  const std::vector<Item> items = sweep_items(tour, g, rr_task, cross);
+  const std::vector<Group> groups = issue_groups(items);
 
-  // ---- workspaces, metric, exchange buffers, cross-stream events
+  // ---- workspaces (one per chain), metric, per-half receive buffers, events
   const size_t wsb = svdj_block_workspace_bytes(p->dtype, W, k / 2, p->m_pad);
-  void *ws_a = nullptr, *ws_b = nullptr, *rA = nullptr, *rV = nullptr, *rD = nullptr;
+  void* ws[2] = {nullptr, nullptr};
+  void *rA[2] = {nullptr, nullptr}, *rV[2] = {nullptr, nullptr}, *rD[2] = {nullptr, nullptr};
   uint32_t* metric = nullptr;
-  HIPC(hipMalloc(&ws_a, wsb));
-  HIPC(hipMalloc(&ws_b, wsb));
-  HIPC(hipMalloc((void**)&metric, 2 * sizeof(uint32_t)));
-  HIPC(hipMalloc(&rA, (size_t)B * p->m_pad * es));
-  HIPC(hipMalloc(&rD, (size_t)B * es));
-  if (p->Vt) HIPC(hipMalloc(&rV, (size_t)B * p->n_v * es));
-  hipEvent_t ea, eb;
-  HIPC(hipEventCreateWithFlags(&ea, hipEventDisableTiming));
-  HIPC(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
-  auto join = [&]() -> int {  // both streams wait for each other
-    HIPC(hipEventRecord(ea, sa));
-    HIPC(hipEventRecord(eb, sb));
-    HIPC(hipStreamWaitEvent(sa, eb, 0));
-    HIPC(hipStreamWaitEvent(sb, ea, 0));
-    return 0;
+  hipStream_t sc = (hipStream_t)p->stream_comm;
+  const bool own_sc = sc == nullptr && P > 1;
+  std::vector<hipEvent_t> ev(items.size() + 4, nullptr);  // per item + ready, join, copied[2]
+  auto alloc = [&](void** q, size_t bytes) {
+    if (!rc && hipMalloc(q, bytes) != hipSuccess) rc = fail(-100, "hipMalloc(%zu) failed", bytes);
   };
-  auto phase = [&](const Task& a, const Task& b) -> int {
-    SVDJC(svdj_block_steps2(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
-                            a.pairs, a.npairs, a.steps, a.modes.data(), ws_a, wsb, sa, b.pairs,
-                            b.npairs, b.steps, b.modes.data(), ws_b, wsb, sb, p->tol, p->tol_mode,
-                            1, metric, p->mma));
-    return join();
-  };
+  for (int c = 0; c < 2; ++c) alloc(&ws[c], wsb);
+  alloc((void**)&metric, 2 * sizeof(uint32_t));
+  if (P > 1)
+    for (int h = 0; h < 2; ++h) {
+      alloc(&rA[h], (size_t)hB * p->m_pad * es);
+      alloc(&rD[h], (size_t)hB * es);
+      if (p->Vt) alloc(&rV[h], (size_t)hB * p->n_v * es);
+    }
+  if (!rc && own_sc && hipStreamCreateWithFlags(&sc, hipStreamNonBlocking) != hipSuccess)
+    rc = fail(-100, "comm stream creation failed");
+  for (auto& e : ev)
+    if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      rc = fail(-100, "event creation failed");
+  hipEvent_t ev_ready = ev[items.size()], ev_join = ev[items.size() + 1];
+  hipEvent_t* ev_copied = &ev[items.size() + 2];
 
   // placement of every GPU's slots (all ranks simulate the whole table)
   std::vector<int32_t> phys(2 * P);
@@ -225,56 +345,118 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     phys[2 * h] = tour.h(0, h, 0);
     phys[2 * h + 1] = tour.h(0, h, 1);
   }
-  if (p->held[0] != phys[2 * g] || p->held[1] != phys[2 * g + 1])
-    return fail(-2, "rank %d holds (%d, %d), the tournament starts from (%d, %d)", g, p->held[0],
-                p->held[1], phys[2 * g], phys[2 * g + 1]);
-  int rc = 0;
-  p->sweeps = 0;
-  p->converged = 0;
-  for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
+  if (!rc && (p->held[0] != phys[2 * g] || p->held[1] != phys[2 * g + 1]))
+    rc = fail(-2, "rank %d holds (%d, %d), the tournament starts from (%d, %d)", g, p->held[0],
+              p->held[1], phys[2 * g], phys[2 * g + 1]);
+
+  auto rows = [&](int slot, int half) { return (size_t)slot * B + (size_t)half * hB; };
+  // One sweep: every dependency is an event; the host never waits.
+  auto sweep = [&]() -> int {
+    std::vector<hipEvent_t> last[4];   // task events on each half since its last exchange
+    hipEvent_t pending[4] = {nullptr, nullptr, nullptr, nullptr};  // arrived, not copied in
+    bool copied_used[2] = {false, false};
+    int halves_sent = 0;
     HIPC(hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), sa));
-    if ((rc = join())) break;
-    if ((rc = phase(rr_task[0], rr_task[1]))) break;
-    for (int r = 0; r < tour.R && !rc; ++r) {
-      const int inc = r == 0 ? 0 : tour.x(r, g);
-      if ((rc = phase(cross[inc][0][0], cross[inc][1][1]))) break;
-      if ((rc = phase(cross[inc][0][1], cross[inc][1][0]))) break;
-      if (r + 1 < tour.R) {  // exchange before round r+1, on stream a (b waits below)
-        const int x = tour.x(r + 1, g), dst = tour.to(r + 1, g), src = tour.from(r + 1, g);
-        char* A0 = (char*)p->At + (size_t)x * B * p->m_pad * es;
-        char* D0 = (char*)p->D + (size_t)x * B * es;
+    HIPC(hipEventRecord(ev_ready, sa));
+    HIPC(hipStreamWaitEvent(st[1], ev_ready, 0));
+    if (sc) HIPC(hipStreamWaitEvent(sc, ev_ready, 0));
+    auto consume = [&](int hv, hipStream_t s) -> int {
+      if (!pending[hv]) return 0;
+      HIPC(hipStreamWaitEvent(s, pending[hv], 0));
+      pending[hv] = nullptr;
+      const int slot = hv / 2, half = hv % 2;
+      const size_t r0 = rows(slot, half);
+      HIPC(hipMemcpyAsync((char*)p->At + r0 * p->m_pad * es, rA[half], (size_t)hB * p->m_pad * es,
+                          hipMemcpyDeviceToDevice, s));
+      HIPC(hipMemcpyAsync((char*)p->D + r0 * es, rD[half], (size_t)hB * es, hipMemcpyDeviceToDevice, s));
+      if (p->Vt)
+        HIPC(hipMemcpyAsync((char*)p->Vt + r0 * p->n_v * es, rV[half], (size_t)hB * p->n_v * es,
+                            hipMemcpyDeviceToDevice, s));
+      HIPC(hipEventRecord(ev_copied[half], s));  // the next receive into rV[half] waits on it
+      copied_used[half] = true;
+      return 0;
+    };
+    for (const Group& gr : groups) {
+      const Item& a = items[gr.a];
+      if (a.send) {  // one half of slot a.slot to send_to, its replacement from recv_from
+        const int key = a.slot * 2 + a.half, dst = tour.to(a.round, g), src = tour.from(a.round, g);
+        for (hipEvent_t e : last[key]) HIPC(hipStreamWaitEvent(sc, e, 0));
+        last[key].clear();
+        if (copied_used[a.half]) HIPC(hipStreamWaitEvent(sc, ev_copied[a.half], 0));
+        const size_t r0 = rows(a.slot, a.half);
         NCCLC(ncclGroupStart());
-        NCCLC(ncclSend(A0, (size_t)B * p->m_pad, nt, dst, comm, sa));
-        NCCLC(ncclSend(D0, (size_t)B, nt, dst, comm, sa));
-        NCCLC(ncclRecv(rA, (size_t)B * p->m_pad, nt, src, comm, sa));
-        NCCLC(ncclRecv(rD, (size_t)B, nt, src, comm, sa));
+        NCCLC(ncclSend((char*)p->At + r0 * p->m_pad * es, (size_t)hB * p->m_pad, nt, dst, comm, sc));
+        NCCLC(ncclSend((char*)p->D + r0 * es, (size_t)hB, nt, dst, comm, sc));
+        NCCLC(ncclRecv(rA[a.half], (size_t)hB * p->m_pad, nt, src, comm, sc));
+        NCCLC(ncclRecv(rD[a.half], (size_t)hB, nt, src, comm, sc));
         if (p->Vt) {
-          char* V0 = (char*)p->Vt + (size_t)x * B * p->n_v * es;
-          NCCLC(ncclSend(V0, (size_t)B * p->n_v, nt, dst, comm, sa));
-          NCCLC(ncclRecv(rV, (size_t)B * p->n_v, nt, src, comm, sa));
+          NCCLC(ncclSend((char*)p->Vt + r0 * p->n_v * es, (size_t)hB * p->n_v, nt, dst, comm, sc));
+          NCCLC(ncclRecv(rV[a.half], (size_t)hB * p->n_v, nt, src, comm, sc));
         }
         NCCLC(ncclGroupEnd());
-        HIPC(hipMemcpyAsync(A0, rA, (size_t)B * p->m_pad * es, hipMemcpyDeviceToDevice, sa));
-        HIPC(hipMemcpyAsync(D0, rD, (size_t)B * es, hipMemcpyDeviceToDevice, sa));
-        if (p->Vt)
-          HIPC(hipMemcpyAsync((char*)p->Vt + (size_t)x * B * p->n_v * es, rV,
-                              (size_t)B * p->n_v * es, hipMemcpyDeviceToDevice, sa));
-        if ((rc = join())) break;
-        std::vector<int32_t> old = phys;
-        for (int h = 0; h < P; ++h) {
-          const int sh = tour.from(r + 1, h);
-          phys[2 * h + tour.x(r + 1, h)] = old[2 * sh + tour.x(r + 1, sh)];
+        hipEvent_t arrived = ev[gr.a];
+        HIPC(hipEventRecord(arrived, sc));
+        pending[key] = arrived;
+        if (++halves_sent % 2 == 0) {  // both halves of round a.round issued: new placement
+          std::vector<int32_t> old = phys;
+          for (int h = 0; h < P; ++h) {
+            const int sh = tour.from(a.round, h);
+            phys[2 * h + tour.x(a.round, h)] = old[2 * sh + tour.x(a.round, sh)];
+          }
+        }
+        continue;
+      }
+      const int n_t = gr.b < 0 ? 1 : 2;
+      const Item* t[2] = {&a, gr.b < 0 ? nullptr : &items[gr.b]};
+      for (int q = 0; q < n_t; ++q) {
+        hipStream_t s = st[t[q]->stream];
+        for (int hv : t[q]->hv) {
+          for (hipEvent_t e : last[hv]) HIPC(hipStreamWaitEvent(s, e, 0));
+          if (int r2 = consume(hv, s)) return r2;
         }
       }
+      const Task &x = *t[0]->task;
+      if (n_t == 2) {
+        const Task& y = *t[1]->task;
+        const int cx = t[0]->stream, cy = t[1]->stream;
+        SVDJC(svdj_block_steps2(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
+                                x.pairs, x.npairs, x.steps, x.modes.data(), ws[cx], wsb, st[cx],
+                                y.pairs, y.npairs, y.steps, y.modes.data(), ws[cy], wsb, st[cy],
+                                p->tol, p->tol_mode, 1, metric, p->mma));
+      } else {
+        const int cx = t[0]->stream;
+        SVDJC(svdj_block_steps(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
+                               x.pairs, x.npairs, x.steps, x.modes.data(), p->tol, p->tol_mode, 1,
+                               ws[cx], wsb, metric, p->mma, st[cx]));
+      }
+      for (int q = 0; q < n_t; ++q) {
+        hipEvent_t e = ev[q == 0 ? gr.a : gr.b];
+        HIPC(hipEventRecord(e, st[t[q]->stream]));
+        for (int hv : t[q]->hv) last[hv].push_back(e);
+      }
     }
-    if (rc) break;
+    HIPC(hipEventRecord(ev_join, st[1]));
+    HIPC(hipStreamWaitEvent(sa, ev_join, 0));
+    return 0;
+  };
+
+  if (!rc) {
+    p->sweeps = 0;
+    p->converged = 0;
+  }
+  for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
+    if ((rc = sweep())) break;
     // ---- stop test: global max convergence value (positive floats order as
     // uint32) and total rotated pairs
-    NCCLC(ncclAllReduce(metric, metric, 1, ncclUint32, ncclMax, comm, sa));
-    NCCLC(ncclAllReduce(metric + 1, metric + 1, 1, ncclUint32, ncclSum, comm, sa));
-    uint32_t hm[2];
-    HIPC(hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
-    HIPC(hipStreamSynchronize(sa));
+    uint32_t hm[2] = {0, 0};
+    auto reduce = [&]() -> int {
+      NCCLC(ncclAllReduce(metric, metric, 1, ncclUint32, ncclMax, comm, sa));
+      NCCLC(ncclAllReduce(metric + 1, metric + 1, 1, ncclUint32, ncclSum, comm, sa));
+      HIPC(hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
+      HIPC(hipStreamSynchronize(sa));
+      return 0;
+    };
+    if ((rc = reduce())) break;
     float mx;
     memcpy(&mx, &hm[0], sizeof(float));
     if (p->hist) p->hist[sw] = mx;
@@ -292,18 +474,22 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
       if (r2 < 0) rc = fail(r2, "finalize: %s", svdj_hip_last_error());
     }
     if (!rc && hipStreamSynchronize(sa) != hipSuccess) rc = fail(-100, "final sync failed");
+  } else {
+    (void)hipDeviceSynchronize();  // nothing of this call may still run on its buffers
   }
-  (void)hipEventDestroy(ea);
-  (void)hipEventDestroy(eb);
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (own_sc && sc) (void)hipStreamDestroy(sc);
   for (auto* t : {&rr_task[0], &rr_task[1]}) (void)hipFree(t->pairs);
   for (auto& a : cross)
     for (auto& b : a)
       for (auto& c : b) (void)hipFree(c.pairs);
-  (void)hipFree(ws_a);
-  (void)hipFree(ws_b);
+  for (int h = 0; h < 2; ++h) {
+    (void)hipFree(ws[h]);
+    (void)hipFree(rA[h]);
+    (void)hipFree(rD[h]);
+    (void)hipFree(rV[h]);
+  }
   (void)hipFree(metric);
-  (void)hipFree(rA);
-  (void)hipFree(rD);
-  (void)hipFree(rV);
   return rc;
 }

@@ -4,9 +4,10 @@
 // with no Python and no MPI.
 //
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
-//                  [--dtype f32|f64] [--block W] [--max-sweeps K] [--tol T]
+//                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
 //                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--no-v]
-//                  [--shared-gpu] [--verify] [--timeout SEC] [--id-file PATH]
+//                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
+//                  [--id-file PATH]
 //
 // The launcher forks P ranks before anything touches the GPU (the parent never
 // does) and waits for them; a rank that fails or a job that exceeds --timeout
@@ -44,7 +45,7 @@
 namespace {
 
 struct Opts {
-  int n = 0, m = 0, np = 0, W = 32, max_sweeps = 60, mma = 0;
+  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
   bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;
@@ -75,6 +76,14 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   const int dtype = sizeof(T) == 8 ? 1 : 0;
   const ncclDataType_t nt = dtype ? ncclFloat64 : ncclFloat32;
   CK(hipSetDevice(device));
+  // The chain and exchange streams are created first: HIP maps streams onto
+  // GPU_MAX_HW_QUEUES hardware queues as they are created, and streams made
+  // after RCCL's internal ones were seen to share one queue (the chains then
+  // serialise: rocprofv3 queue ids, profiles/r2_native_dist).
+  hipStream_t sa, sb, sc;
+  CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&sc, hipStreamNonBlocking));
   void* comm = nullptr;
   if (svdj_dist_comm_init(rank, world, o.id_file.c_str(), o.timeout, &comm) < 0) {
     std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
@@ -82,8 +91,9 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   }
   ncclComm_t nc = (ncclComm_t)comm;
   const int m = o.m, n = o.n;
+  const int W = o.W ? o.W : svdj_dist_choose_block(dtype, world, n);
   int B, ncols, m_pad, n_v;
-  if (svdj_dist_geometry(world, m, n, o.W, &B, &ncols, &m_pad, &n_v) < 0) {
+  if (svdj_dist_geometry(world, m, n, W, &B, &ncols, &m_pad, &n_v) < 0) {
     std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
     return 1;
   }
@@ -105,9 +115,6 @@ int run_rank(const Opts& o, int rank, int world, int device) {
     }
   if (rank != 0 || !o.verify) std::vector<double>().swap(A);
 
-  hipStream_t sa, sb;
-  CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
-  CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
   T *dA, *dV = nullptr, *dD, *dS;
   double* dt;
   CK(hipMalloc((void**)&dA, hA.size() * sizeof(T)));
@@ -115,60 +122,65 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   CK(hipMalloc((void**)&dD, (size_t)2 * B * sizeof(T)));
   CK(hipMalloc((void**)&dS, (size_t)2 * B * sizeof(T)));
   CK(hipMalloc((void**)&dt, sizeof(double)));
-  CK(hipMemcpy(dA, hA.data(), hA.size() * sizeof(T), hipMemcpyHostToDevice));
   double tol = o.tol;
   if (tol <= 0)  // sqrt(m) eps (LAPACK xGESVJ), as utils/metrics.py default_tol
     tol = std::sqrt((double)m) * (dtype ? 2.220446049250313e-16 : 1.1920929e-07);
-
-  // ---- timed region: V = I, column norms, sweeps, sigma / U normalisation
-  NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclSum, nc, sa));  // barrier
-  CK(hipStreamSynchronize(sa));
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int s = 0; s < 2 && o.want_v; ++s)
-    if (svdj_set_identity(dtype, dV + (size_t)s * B * n_v, n_v, n_v, B, held[s] * B, sa) < 0) {
-      std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
-      return 2;
-    }
-  if (svdj_col_norms2(dtype, dA, m_pad, m_pad, 2 * B, dD, sa) < 0) {
-    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
-    return 2;
-  }
   std::vector<double> hist(o.max_sweeps, 0.0);
   svdj_dist_problem p{};
   p.rank = rank;
   p.world = world;
   p.comm = comm;
   p.dtype = dtype;
-  p.W = o.W;
+  p.W = W;
   p.m_pad = m_pad;
   p.n_v = n_v;
   p.B = B;
   p.At = dA;
   p.Vt = dV;
   p.D = dD;
-  p.held[0] = held[0];
-  p.held[1] = held[1];
   p.tol = tol;
   p.tol_mode = o.abs_tol ? 1 : 0;
   p.max_sweeps = o.max_sweeps;
   p.mma = o.mma;
   p.stream_a = sa;
   p.stream_b = sb;
+  p.stream_comm = sc;
   p.hist = hist.data();
-  if (svdj_dist_solve(&p, dS) < 0) {
-    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
-    return 2;
+  double secs = 0;
+  // --warmup solves first (RCCL connects its peers lazily, on the first
+  // send/recv), then the timed one; each starts from the original columns
+  for (int it = 0; it <= o.warmup; ++it) {
+    CK(hipMemcpy(dA, hA.data(), hA.size() * sizeof(T), hipMemcpyHostToDevice));
+    p.held[0] = held[0];
+    p.held[1] = held[1];
+    // ---- timed region: V = I, column norms, sweeps, sigma / U normalisation
+    NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclSum, nc, sa));  // barrier
+    CK(hipStreamSynchronize(sa));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int s = 0; s < 2 && o.want_v; ++s)
+      if (svdj_set_identity(dtype, dV + (size_t)s * B * n_v, n_v, n_v, B, held[s] * B, sa) < 0) {
+        std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
+        return 2;
+      }
+    if (svdj_col_norms2(dtype, dA, m_pad, m_pad, 2 * B, dD, sa) < 0) {
+      std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
+      return 2;
+    }
+    if (svdj_dist_solve(&p, dS) < 0) {
+      std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
+      return 2;
+    }
+    secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    CK(hipMemcpy(dt, &secs, sizeof(double), hipMemcpyHostToDevice));
+    NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, nc, sa));
+    CK(hipMemcpyAsync(&secs, dt, sizeof(double), hipMemcpyDeviceToHost, sa));
+    CK(hipStreamSynchronize(sa));
   }
-  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  CK(hipMemcpy(dt, &secs, sizeof(double), hipMemcpyHostToDevice));
-  NK(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, nc, sa));
-  CK(hipMemcpyAsync(&secs, dt, sizeof(double), hipMemcpyDeviceToHost, sa));
-  CK(hipStreamSynchronize(sa));
 
   if (rank == 0) {
     std::printf("%s\n", svdj_hip_version());
     std::printf("Dimensions, height: %d, width: %d\n", m, n);
-    std::printf("ranks: %d  block W: %d  super-block B: %d  %s\n", world, o.W, B,
+    std::printf("ranks: %d  block W: %d  super-block B: %d  %s\n", world, W, B,
                 o.shared ? "(shared GPU)" : "");
     std::printf("SVD MPI+OMP time with U,V calculation: %.6f\n", secs);
     std::printf("sweeps: %d  converged: %d  last off value: %.3e  tol: %.3e\n", p.sweeps,
@@ -296,7 +308,7 @@ int rank_main(const Opts& o, int rank, int world, int local) {
 
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s N --np P [--m M] [--dtype f32|f64] [--block W] [--shared-gpu] [--verify] ...\n",
+    std::fprintf(stderr, "usage: %s N --np P [--m M] [--dtype f32|f64] [--block W (default: per-GPU size)] [--shared-gpu] [--verify] ...\n",
                  argv[0]);
     return 1;
   }
@@ -320,6 +332,7 @@ int main(int argc, char** argv) {
     else if (a == "--shared-gpu") o.shared = true;
     else if (a == "--verify") o.verify = true;
     else if (a == "--timeout") o.timeout = std::atof(next());
+    else if (a == "--warmup") o.warmup = std::atoi(next());
     else if (a == "--id-file") o.id_file = next();
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());

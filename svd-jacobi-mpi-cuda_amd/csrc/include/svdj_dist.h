@@ -5,12 +5,12 @@
 // driven from main.cu:1587; lib/JacobiMethods.cuh:44-52).  This is the
 // MI355X-native equivalent without Python: the super-block tournament of
 // svdj_tournament (2P super-blocks, 2P-1 rounds, one super-block exchanged
-// per GPU per round with grouped ncclSend/ncclRecv), the block steps of
-// libsvdj_hip on two staggered chains per phase, and an RCCL all-reduce of
-// the sweep's convergence value and rotation count as the stop test.  The
-// Python solver (parallel/distributed.py) additionally pipelines the exchange
-// in half super-blocks under the compute; this native path exchanges whole
-// super-blocks between rounds.
+// per GPU per round), the block steps of libsvdj_hip on two staggered chains,
+// and an RCCL all-reduce of the sweep's convergence value and rotation count
+// as the stop test.  The exchange is pipelined as in parallel/pipeline.py:
+// each super-block moves in two halves with grouped ncclSend/ncclRecv on a
+// comm stream as soon as the tasks touching that half are done, and consumers
+// wait on the arrival event -- the host never blocks inside a sweep.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -31,6 +31,10 @@ int svdj_dist_comm_destroy(void* comm);
 // super-blocks of B columns (B/W even); row counts padded to 128.
 int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* ncols, int* m_pad, int* n_v);
 
+// Default block width (models/block.py choose_block on the per-GPU column
+// count n / world): 64 from 12288 columns per GPU on, else 32.
+int svdj_dist_choose_block(int dtype, int world, int n);
+
 // Super-block ids held by `rank` at the start of a sweep (round 0 placement).
 int svdj_dist_initial_held(int world, int rank, int32_t held[2]);
 
@@ -50,6 +54,10 @@ typedef struct {
   int mma;                    // matrix-core mode of the apply (svdj_block_steps)
   void* stream_a;             // two compute streams (distinct)
   void* stream_b;
+  void* stream_comm;          // exchange stream, or NULL (created per call).  HIP maps
+                              // streams onto GPU_MAX_HW_QUEUES hardware queues as they
+                              // are created: make the three streams first, before RCCL's
+                              // own, or two of them may share a queue and serialise.
   double* hist;               // host [max_sweeps]: per-sweep global max convergence value
   int sweeps;                 // out
   int converged;              // out
@@ -59,6 +67,12 @@ typedef struct {
 // normalises U in place (At rows) and writes sigma[2B] (device, data type).
 // Collective: every rank calls it.  Returns 0 or <0 (svdj_dist_last_error()).
 int svdj_dist_solve(svdj_dist_problem* p, void* sigma);
+
+// Issue order of one sweep on `rank` (host only, for tests): per group 7 ints
+// {kind, ...}: kind 0 = one task {stream, half, half}, 1 = a staggered pair
+// {stream, half, half, stream, half, half}, 2 = a half exchange {round, slot,
+// half}; halves are slot*2 + half.  Returns the group count (<= cap) or <0.
+int svdj_dist_plan(int world, int rank, int32_t* out, int cap);
 
 // Message of the calling thread's last failure.
 const char* svdj_dist_last_error(void);

@@ -70,3 +70,42 @@ def test_stagger_groups_keep_coverage(P, k):
         regrouped.append(new)
     pipeline.check_plan_coverage(regrouped, tour)
     assert pipeline.issue_groups(plans[0].items, False) == plans[0].items
+
+
+def _native_plan(P, g):
+    import ctypes
+    import importlib
+    import numpy as np
+    b = importlib.import_module("svd-jacobi-mpi-cuda_amd._build")
+    try:
+        b.build_dist()
+    except (FileNotFoundError, RuntimeError) as e:  # no hipcc / rccl in this environment
+        pytest.skip(f"native distributed library not buildable here: {e}")
+    lib = ctypes.CDLL(str(b.DIST_LIB))
+    out = np.zeros((4096, 7), dtype=np.int32)
+    n = lib.svdj_dist_plan(P, g, out.ctypes.data_as(ctypes.c_void_p), out.shape[0])
+    assert n > 0
+    return out[:n].tolist()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_native_plan_matches_python(P):
+    """csrc/dist/svdj_dist.cpp builds the same sweep and issue order as the
+    Python executor (sweep_plan + issue_groups) on every rank."""
+    tour = schedule.tournament(P)
+
+    def hv(x):
+        return [s * 2 + h for s, h in x.halves]
+
+    for g in range(P):
+        groups = pipeline.issue_groups(pipeline.sweep_plan(P, 4, tour.xslot[:, g]).items, True)
+        want = []
+        for it in groups:
+            if isinstance(it, pipeline.Send):
+                want.append([2, it.round, it.slot, it.half, -1, -1, -1])
+            elif isinstance(it, tuple):
+                a, b_ = it
+                want.append([1, a.stream, *hv(a), b_.stream, *hv(b_)])
+            else:
+                want.append([0, it.stream, *hv(it), -1, -1, -1])
+        assert _native_plan(P, g) == want
