@@ -148,9 +148,10 @@ extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* n
   return 0;
 }
 
-extern "C" int svdj_dist_choose_block(int dtype, int world, int n) {
-  (void)dtype;  // same crossover for fp32 and fp64 (models/block.py measurements)
-  return n / (world > 0 ? world : 1) >= 12288 ? 64 : 32;
+extern "C" int svdj_dist_choose_block(int dtype, int world, int m, int n) {
+  (void)dtype;  // same crossover for fp32 and fp64 (models/block.py choose_block)
+  const int per_gpu = n / (world > 0 ? world : 1);
+  return (m >= 12288 && per_gpu >= 4096) ? 64 : 32;
 }
 
 extern "C" int svdj_dist_initial_held(int world, int rank, int32_t held[2]) {

@@ -91,7 +91,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   }
   ncclComm_t nc = (ncclComm_t)comm;
   const int m = o.m, n = o.n;
-  const int W = o.W ? o.W : svdj_dist_choose_block(dtype, world, n);
+  const int W = o.W ? o.W : svdj_dist_choose_block(dtype, world, m, n);
   int B, ncols, m_pad, n_v;
   if (svdj_dist_geometry(world, m, n, W, &B, &ncols, &m_pad, &n_v) < 0) {
     std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());

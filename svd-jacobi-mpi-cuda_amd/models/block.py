@@ -17,17 +17,21 @@ from .base import SVDResult, Solver, Timer
 
 
 def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
-    if dtype == torch.float64:
-        # fp64: the apply is MFMA-bound from W=32 on, W=64 halves the steps.
-        # Measured (MI355X, s per solve W=32 / W=64): 8192: 2.50 / 2.92,
-        # 16384: 17.8 / 16.5 (profiles/r2_configs).
-        return 64 if n >= 12288 else 32
-    # fp32: W=64 halves the per-byte traffic of the Gram and needs half the
-    # steps, but its EVD is 4.5x slower (280 vs 62 us).  Measured with the
-    # staggered chains (MI355X, n x n, s per solve W=32 / W=64): 2048: 0.087 /
-    # 0.160, 4096: 0.27 / 0.40, 8192: 1.23 / 1.31, 16384: 9.07 / 6.81.  ``n``
-    # is the per-GPU column count (distributed callers pass n / P).
-    return 64 if n >= 12288 else 32
+    """Block width W for ``n`` columns per GPU of ``m`` rows.
+
+    W=64 halves the steps and the per-byte traffic of the Gram and the apply
+    but its EVD is ~4x slower (190 vs 45 us), and it halves the number of
+    pairs a step can run at once.  It pays when the rows are long (the
+    apply / Gram dominate) and there are still >= 16 pairs per half task.
+    Measured on MI355X (profiles/r2_configs, profiles/r2_simgrid):
+      * 1 GPU n x n, s per solve W=32 / W=64: fp32 8192: 1.23 / 1.31,
+        16384: 9.07 / 6.81; fp64 8192: 2.50 / 2.92, 16384: 17.8 / 16.5.
+      * rank plan of the 16384^2 fp32 job, ms per sweep W=32 / W=64: P=2
+        (8192 columns per GPU): 354 / 244, P=4 (4096): 187 / 155, P=8 (2048):
+        93 / 115.
+    """
+    del dtype  # same crossover for fp32 and fp64 (see the measurements above)
+    return 64 if (m >= 12288 and n >= 4096) else 32
 
 
 class BlockJacobi(Solver):
