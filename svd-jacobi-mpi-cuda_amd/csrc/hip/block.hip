@@ -24,6 +24,7 @@
 #include "common.hpp"
 #include "svdj_hip.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -825,9 +826,16 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 #ifndef SVDJ_APPLY_THREADS_64
 #define SVDJ_APPLY_THREADS_64 256
 #endif
+#ifndef SVDJ_APPLY_THREADS_32
+#define SVDJ_APPLY_THREADS_32 256
+#endif
+#ifndef SVDJ_APPLY_EARLY
+#define SVDJ_APPLY_EARLY 0
+#endif
 template <typename T, int W>
 __host__ __device__ constexpr int apply_threads() {
-  return (W == 64 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_64 : kApplyThreads;
+  return (W == 64 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_64
+                                     : ((W == 32 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_32 : kApplyThreads);
 }
 template <typename T, int W>
 __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
@@ -863,10 +871,6 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     r_begin = chunk * rows_v;
     r_end = min(n_v, r_begin + rows_v);
   }
-  const T* Qg = Qall + (size_t)pair * N * N;
-  for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
-  __syncthreads();
-
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lc = M::lane_col(lane), kg = M::lane_kg(lane);
   // Column k of X = [A_bi A_bj] is base + col(k)*ld.  The lane-dependent
@@ -890,9 +894,18 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     }
   };
   int r0 = r_begin + wave * TL;
-  if (r0 >= r_end) return;
   T xv[NK];
+#if SVDJ_APPLY_EARLY
+  // the first X tile is independent of Q: its HBM latency overlaps the Q fill
+  if (r0 < r_end) load_tile(xv, r0);
+#endif
+  const T* Qg = Qall + (size_t)pair * N * N;
+  for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
+  __syncthreads();
+  if (r0 >= r_end) return;
+#if !SVDJ_APPLY_EARLY
   load_tile(xv, r0);
+#endif
   while (true) {
     const int rn = r0 + WAVES * TL;
     const bool more = rn < r_end;
@@ -1113,7 +1126,10 @@ static Geometry make_geometry(int P, int m_pad, int n_v) {
   g.gchunks = (m_pad + g.grows - 1) / g.grows;
   // Apply: ~1024+ workgroups over A and V rows, >= 128 rows each.
   int total_rows = m_pad + n_v;
-  int wg_target = 2048;
+  static const int wg_target = [] {
+    const char* e = getenv("SVDJ_APPLY_WG_TARGET");  // tuning experiments only
+    return e && atoi(e) > 0 ? atoi(e) : 2048;
+  }();
   int rows = round_up((int)(((long)total_rows * P + wg_target - 1) / wg_target), 128);
   if (rows < 128) rows = 128;
   if (rows > 2048) rows = 2048;
