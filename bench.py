@@ -197,7 +197,8 @@ def simulate(a, cfg, dtype, work):
         "simulated_P": P, "simulated_rank": g, "sweeps_run": res.sweeps,
         "solve_s": round(el, 4), "dtype": a.dtype,
         "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
-                   "chains": a.chains, "link_gbps_model": a.sim_link_gbps},
+                   "chains": a.chains, "inner_order": a.inner_order,
+                   "link_gbps_model": a.sim_link_gbps},
         "comm": res.info.get("comm"),
         "qr_seconds": res.info.get("qr_seconds"),
         "sim_bytes_per_exchange": comm.bytes_moved // max(comm.exchanges, 1),
@@ -208,6 +209,11 @@ def simulate(a, cfg, dtype, work):
     if a.json_out:
         with open(a.json_out, "w") as f:
             json.dump(line, f)
+
+
+def svdj_default_inner() -> str:
+    import svdj
+    return svdj.SolverConfig().inner_order
 
 
 def main():
@@ -226,6 +232,8 @@ def main():
     p.add_argument("--tol", type=float, default=None,
                    help="rotation threshold (default sqrt(m) eps of the problem dtype)")
     p.add_argument("--chains", type=int, default=2)
+    p.add_argument("--inner-order", default=svdj_default_inner(), choices=["cyclic", "bipartite"],
+                   help="EVD ordering of the block cross steps")
     p.add_argument("--no-stagger", action="store_true",
                    help="issue the two step chains independently (lockstep) instead of offset")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
@@ -256,6 +264,7 @@ def main():
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps, tol=a.tol,
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
                             stagger=not a.no_stagger, precondition=a.precondition,
+                            inner_order=a.inner_order,
                             progress=a.progress, comm_timing=a.gpus > 1)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
@@ -342,6 +351,7 @@ def main():
                 "mma": last.info.get("mma", a.mma),
                 "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
+                "inner_order": a.inner_order,
                 "staggered": not a.no_stagger,
                 "root_owned": a.root_owned,
             },

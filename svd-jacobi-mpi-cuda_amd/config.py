@@ -50,6 +50,8 @@ class SolverConfig:
     tol_mode: str = "relative"      # relative | absolute (reference parity)
     max_sweeps: int = 60            # reference: 1 (main.cu:482)
     max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)
+    inner_order: str = "cyclic"     # block path, cross steps: cyclic (2W-1 EVD steps, all
+                                    # pairs) | bipartite (W steps, cross pairs only)
     ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
@@ -105,6 +107,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--tol-mode", default="relative", choices=["relative", "absolute"])
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--max-inner-sweeps", type=int, default=1)
+    p.add_argument("--inner-order", default=None, choices=["cyclic", "bipartite"],
+                   help="EVD ordering of the block cross steps (default: the config's)")
     p.add_argument("--ordering", default="sameh", choices=["sameh", "round_robin"])
     p.add_argument("--sort", action="store_true")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"])
@@ -121,4 +125,6 @@ def config_from_args(a) -> SolverConfig:
                         max_inner_sweeps=a.max_inner_sweeps, ordering=a.ordering, sort=a.sort,
                         mma=a.mma, precondition=a.precondition, checkpoint_dir=a.checkpoint_dir,
                         checkpoint_every=a.checkpoint_every,
-                        progress=bool(getattr(a, "progress", False)))
+                        progress=bool(getattr(a, "progress", False)),
+                        **({"inner_order": a.inner_order}
+                           if getattr(a, "inner_order", None) else {}))

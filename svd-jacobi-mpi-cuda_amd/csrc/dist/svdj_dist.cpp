@@ -290,7 +290,8 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   std::vector<int32_t> rr((size_t)(k - 1) * (k / 2) * 2);
   svdj_round_robin(k, rr.data());
   Task rr_task[2], cross[2][2][2];  // cross[incoming slot][I half][S half]
-  std::vector<int32_t> rr_modes(k - 1, 0);
+  const int cross_mode = p->inner_order ? 2 : 0;  // svdj_block_steps mode of a cross step
+  std::vector<int32_t> rr_modes(k - 1, cross_mode);
   rr_modes[0] = 1;  // the first step of a sweep re-measures the diagonal (full Gram)
   int rc = 0;
   for (int s = 0; s < 2 && !rc; ++s) {
@@ -308,7 +309,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
             h[(t * hk + a) * 2] = inc * k + ih * hk + a;
             h[(t * hk + a) * 2 + 1] = stay * k + sh * hk + (a + t) % hk;
           }
-        rc = upload(cross[inc][ih][sh], h, hk, hk, std::vector<int32_t>(hk, 0));
+        rc = upload(cross[inc][ih][sh], h, hk, hk, std::vector<int32_t>(hk, cross_mode));
       }
   const std::vector<Item> items = sweep_items(tour, g, rr_task, cross);
   const std::vector<Group> groups = issue_groups(items);

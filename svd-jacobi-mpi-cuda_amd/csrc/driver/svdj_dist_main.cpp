@@ -5,7 +5,7 @@
 //
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
-//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--no-v]
+//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH]
 //
@@ -45,7 +45,7 @@
 namespace {
 
 struct Opts {
-  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0;
+  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 0;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
   bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;
@@ -142,6 +142,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.tol_mode = o.abs_tol ? 1 : 0;
   p.max_sweeps = o.max_sweeps;
   p.mma = o.mma;
+  p.inner_order = o.inner;
   p.stream_a = sa;
   p.stream_b = sb;
   p.stream_comm = sc;
@@ -333,6 +334,7 @@ int main(int argc, char** argv) {
     else if (a == "--verify") o.verify = true;
     else if (a == "--timeout") o.timeout = std::atof(next());
     else if (a == "--warmup") o.warmup = std::atoi(next());
+    else if (a == "--inner") o.inner = std::string(next()) == "bipartite" ? 1 : 0;
     else if (a == "--id-file") o.id_file = next();
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());

@@ -5,7 +5,8 @@
 //
 //   svdj_main N [--m M] [--input triu|dense] [--seed S] [--dtype f32|f64]
 //               [--method block|scalar] [--block W] [--max-sweeps K]
-//               [--tol T] [--mma native|bf16x6|bf16x3] [--verify] [--report-dir DIR]
+//               [--tol T] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite]
+//               [--verify] [--report-dir DIR]
 //
 // Prints the reference's lines ("Dimensions, height: .., width: ..",
 // "SVD MPI+OMP time with U,V calculation: ..", "||A-USVt||_F: ..") and writes
@@ -38,7 +39,8 @@ static int rup(int a, int b) { return (a + b - 1) / b * b; }
 
 template <typename T>
 static int run(int m, int n, const std::vector<double>& A0, const std::string& method, int W,
-               int max_sweeps, double tol, int mma, bool verify, const std::string& report_dir) {
+               int max_sweeps, double tol, int mma, int inner_order, bool verify,
+               const std::string& report_dir) {
   const int dtype = sizeof(T) == 8 ? 1 : 0;
   const bool block = method == "block";
   const int ncols = block ? std::max(rup(n, 2 * W), 2 * W) : n;
@@ -74,8 +76,8 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
     CHECK(hipMalloc(&ws, wsb));
     if (svdj_col_norms2(dtype, dA, m_pad, m_pad, ncols, dD, st) < 0) goto fail;
     sweeps = svdj_block_solve(dtype, W, m_pad, dA, m_pad, dV, n_v, n_v, dD, ncols, tol,
-                              /*tol_mode relative*/ 0, 1, max_sweeps, ws, wsb, dmetric,
-                              hist.data(), mma, st);
+                              /*tol_mode relative*/ 0, 1, max_sweeps, inner_order, ws, wsb,
+                              dmetric, hist.data(), mma, st);
   } else {
     const int steps = svdj_sameh_num_steps(n);
     std::vector<int32_t> sched((size_t)steps * (n / 2) * 2);
@@ -142,7 +144,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s N [--m M] [--input triu|dense] [--dtype f32|f64] ...\n", argv[0]);
     return 1;
   }
-  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60;
+  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60, inner_order = 0;
   unsigned seed = 1000000;
   double tol = -1;
   bool verify = false;
@@ -159,6 +161,7 @@ int main(int argc, char** argv) {
     else if (a == "--max-sweeps") max_sweeps = std::atoi(next());
     else if (a == "--tol") tol = std::atof(next());
     else if (a == "--mma") mma = next();
+    else if (a == "--inner") inner_order = std::string(next()) == "bipartite" ? 1 : 0;
     else if (a == "--verify") verify = true;
     else if (a == "--report-dir") report_dir = next();
     else if (a == "--no-report") report_dir.clear();
@@ -176,6 +179,6 @@ int main(int argc, char** argv) {
     svdj_ref_triu_input(m, n, A.data(), m, seed);
   const int mma_code = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
   if (dtype == "f32")
-    return run<float>(m, n, A, method, W, max_sweeps, tol, mma_code, verify, report_dir);
-  return run<double>(m, n, A, method, W, max_sweeps, tol, 0, verify, report_dir);
+    return run<float>(m, n, A, method, W, max_sweeps, tol, mma_code, inner_order, verify, report_dir);
+  return run<double>(m, n, A, method, W, max_sweeps, tol, 0, inner_order, verify, report_dir);
 }

@@ -406,6 +406,122 @@ __host__ __device__ constexpr int block_duty(int a, int b) {  // 256*e + meeting
   return -1;
 }
 
+// ---- inner orderings.  The kernel below is written against an ordering
+// policy: where slot a's two players sit (first_pos / second_pos), how
+// positions move per step (pos_next, prev_pos), which position pairs meet at
+// the next step (next_meeting), the players of a slot at step st, and the
+// register-Q movement (move).
+//   EVD_CYCLIC: the circle-method round robin over all 2W players, 2W-1
+//               steps per sweep (every pair of the 2W x 2W Gram);
+//   EVD_BIP   : the bipartite ordering of the cross pairs only, W steps per
+//               sweep: X players (block i) fixed at positions 0..W-1, the Y
+//               player at Y-position p (position W+p) moves to p-1 (mod W);
+//               slot a pairs positions (a, W+a).  Cross steps of a block
+//               sweep use it (mode 2): the blocks' own columns are mutually
+//               orthogonal when a cross step starts and the full-Gram step
+//               at the start of every sweep rotates the within-block pairs,
+//               so every column pair is still rotated once per sweep at half
+//               the EVD steps (tests/test_schedule.py: bipartite data-flow
+//               emulation; CPU block sweeps: same sweep count +-1).
+enum { EVD_CYCLIC = 0, EVD_BIP = 1 };
+template <int W, int ORD>
+struct Ord;
+template <int W>
+struct Ord<W, EVD_CYCLIC> {
+  static constexpr int R = 2 * W - 1;
+  __host__ __device__ static constexpr int pos_next(int P) { return svdj::pos_next<W>(P); }
+  __host__ __device__ static constexpr int prev_pos(int P) {
+    return P == 2 * W - 1 ? P : (P == 0 ? 2 * W - 2 : P - 1);
+  }
+  __host__ __device__ static constexpr int slot_of(int pos) { return ring_slot_of<W>(pos); }
+  __host__ __device__ static constexpr int next_meeting(int P1, int P2) {
+    return svdj::next_meeting<W>(P1, P2);
+  }
+  __host__ __device__ static constexpr int pos0(int x) { return svdj::pos0<W>(x); }
+  __host__ __device__ static constexpr int first_pos(int a) { return slot_first_pos<W>(a); }
+  __host__ __device__ static constexpr int second_pos(int a) { return slot_second_pos<W>(a); }
+  __host__ __device__ static constexpr int first0(int a) { return a == 0 ? 2 * W - 1 : a; }
+  __host__ __device__ static constexpr int second0(int a) { return a == 0 ? 0 : 2 * W - 1 - a; }
+  __device__ static void players(int a, int st, int& p, int& q) { ring_slot<W>(a, st, p, q); }
+  // firsts shift right, seconds shift left; slot 0's first (player 2W-1)
+  // stays, slot 1 takes slot 0's second, slot W-1's second is its own first
+  template <typename V>
+  __device__ static void move(V& f, V& s, int slot) {
+    const V f_r = dpp_shr1(f), s_r = dpp_shr1(s), s_l = dpp_shl1(s);
+    const V nf = slot == 0 ? f : (slot == 1 ? s_r : f_r);
+    const V ns = slot == W - 1 ? f : s_l;
+    f = nf;
+    s = ns;
+  }
+};
+// Lane i <- lane i+1 with wrap (DPP wave_rol:1).
+__device__ __forceinline__ int dpp_rol1(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x134, 0xf, 0xf, false);
+}
+// Lane i <- lane i ^ 32 (v_permlane32_swap of a value with itself).
+__device__ __forceinline__ int half_swap(int v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+}
+template <int W>
+__device__ __forceinline__ int bip_shift(int v, int slot) {  // slot a <- slot a+1 (mod W)
+  const int r = dpp_rol1(v);
+  if constexpr (W == 32) return slot == W - 1 ? half_swap(r) : r;  // two slot groups per wave
+  return r;
+}
+template <int W>
+__device__ __forceinline__ float bip_shift(float v, int slot) {
+  return __int_as_float(bip_shift<W>(__float_as_int(v), slot));
+}
+template <int W>
+__device__ __forceinline__ double bip_shift(double v, int slot) {
+  const long long x = __double_as_longlong(v);
+  const int lo = bip_shift<W>((int)(x & 0xffffffff), slot), hi = bip_shift<W>((int)(x >> 32), slot);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int W>
+struct Ord<W, EVD_BIP> {
+  static_assert(W == 32 || W == 64 || W <= 16, "bipartite Q movement: one or two slot groups per wave");
+  static constexpr int R = W;
+  __host__ __device__ static constexpr int pos_next(int P) {
+    return P < W ? P : (P == W ? 2 * W - 1 : P - 1);
+  }
+  __host__ __device__ static constexpr int prev_pos(int P) {
+    return P < W ? P : (P == 2 * W - 1 ? W : P + 1);
+  }
+  __host__ __device__ static constexpr int slot_of(int pos) { return pos < W ? pos : pos - W; }
+  __host__ __device__ static constexpr int next_meeting(int P1, int P2) {
+    const int n1 = pos_next(P1), n2 = pos_next(P2);
+    if ((n1 < W) == (n2 < W) || slot_of(n1) != slot_of(n2)) return -1;
+    return 2 * slot_of(n1) + (n1 < W ? 1 : 0);
+  }
+  __host__ __device__ static constexpr int pos0(int x) { return x; }
+  __host__ __device__ static constexpr int first_pos(int a) { return a; }
+  __host__ __device__ static constexpr int second_pos(int a) { return W + a; }
+  __host__ __device__ static constexpr int first0(int a) { return a; }
+  __host__ __device__ static constexpr int second0(int a) { return W + a; }
+  __device__ static void players(int a, int st, int& p, int& q) {
+    p = a;
+    q = W + (a + st) % W;
+  }
+  template <typename V>
+  __device__ static void move(V& f, V& s, int slot) {
+    (void)f;
+    s = bip_shift<W>(s, slot);
+  }
+};
+template <int W, int ORD>
+__host__ __device__ constexpr int block_duty_o(int a, int b) {  // 256*e + meeting, or -1
+  using O = Ord<W, ORD>;
+  for (int e = 0; e < 4; ++e) {
+    const int x = (e >> 1) ? O::second_pos(a) : O::first_pos(a);
+    const int y = (e & 1) ? O::second_pos(b) : O::first_pos(b);
+    const int mt = O::next_meeting(x, y);
+    if (mt >= 0) return 256 * e + mt;
+  }
+  return -1;
+}
+
 // Which slot-pair blocks (a < b) each thread owns, computed at compile time.
 // Thread roles: the W blocks holding the next step's pairs ("duty" blocks:
 // their owners solve the rotations, W = 32 / 64 of them) go to the first W
@@ -414,20 +530,18 @@ __host__ __device__ constexpr int block_duty(int a, int b) {  // 256*e + meeting
 // in complementary pairs 0, W-2, 1, W-3, ... (two paired rows hold W blocks,
 // so a wave's lanes share few slots and the record reads broadcast).
 // blk[j * NT + t] = (a << 8) | b of thread t's j-th block, 0xffff if none.
-template <int W, int NT>
+template <int W, int NT, int ORD = EVD_CYCLIC>
 struct EvdDeal {
   static constexpr int NOFF = W * (W - 1) / 2;
   static constexpr int MAXOFF = (NOFF + NT - 1) / NT;
   unsigned short blk[MAXOFF * NT];
   constexpr EvdDeal() : blk{} {
+    using O = Ord<W, ORD>;
     int g = 0;
     // duty block of each next-step slot s: the positions that slot's players
     // occupy NOW are one behind its own positions
     for (int s = 0; s < W; ++s) {
-      const int f = slot_first_pos<W>(s), q = slot_second_pos<W>(s);
-      const int pf = f == 2 * W - 1 ? f : (f == 0 ? 2 * W - 2 : f - 1);
-      const int pq = q == 0 ? 2 * W - 2 : q - 1;
-      int a = ring_slot_of<W>(pf), b = ring_slot_of<W>(pq);
+      int a = O::slot_of(O::prev_pos(O::first_pos(s))), b = O::slot_of(O::prev_pos(O::second_pos(s)));
       if (a > b) {
         const int x = a;
         a = b;
@@ -438,7 +552,7 @@ struct EvdDeal {
     for (int i = 0; i < W - 1; ++i) {
       const int a = (i & 1) ? W - 2 - (i >> 1) : (i >> 1);
       for (int b = a + 1; b < W; ++b)
-        if (block_duty<W>(a, b) < 0) blk[g++] = (unsigned short)((a << 8) | b);
+        if (block_duty_o<W, ORD>(a, b) < 0) blk[g++] = (unsigned short)((a << 8) | b);
     }
     for (; g < MAXOFF * NT; ++g) blk[g] = 0xffff;
   }
@@ -446,26 +560,28 @@ struct EvdDeal {
 
 // Compile-time check of the dealing: the first W entries are the duty blocks
 // of next-step slots 0..W-1, and every block is dealt exactly once.
-template <int W, int NT>
+template <int W, int NT, int ORD>
 constexpr bool evd_deal_ok() {
-  constexpr EvdDeal<W, NT> d{};
+  constexpr EvdDeal<W, NT, ORD> d{};
   int seen[W * W] = {};
   int dealt = 0;
-  for (int g = 0; g < EvdDeal<W, NT>::MAXOFF * NT; ++g) {
+  for (int g = 0; g < EvdDeal<W, NT, ORD>::MAXOFF * NT; ++g) {
     if (d.blk[g] == 0xffff) continue;
     const int a = d.blk[g] >> 8, b = d.blk[g] & 255;
     if (!(a < b && b < W) || seen[a * W + b]++) return false;
     ++dealt;
-    const int duty = block_duty<W>(a, b);
+    const int duty = block_duty_o<W, ORD>(a, b);
     if (g < W && (duty < 0 || ((duty & 255) >> 1) != g)) return false;
     if (g >= W && duty >= 0) return false;
   }
-  return dealt == EvdDeal<W, NT>::NOFF;
+  return dealt == EvdDeal<W, NT, ORD>::NOFF;
 }
-static_assert(evd_deal_ok<32, evd_threads(32)>() && evd_deal_ok<64, evd_threads(64)>(),
-              "EVD block dealing");
+static_assert(evd_deal_ok<32, evd_threads(32), EVD_CYCLIC>(), "EVD block dealing");
+static_assert(evd_deal_ok<64, evd_threads(64), EVD_CYCLIC>(), "EVD block dealing");
+static_assert(evd_deal_ok<32, evd_threads(32), EVD_BIP>(), "EVD block dealing");
+static_assert(evd_deal_ok<64, evd_threads(64), EVD_BIP>(), "EVD block dealing");
 
-template <typename T, int W>
+template <typename T, int W, int ORD>
 __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     const int32_t* __restrict__ pairs, int full, const T* __restrict__ slabs, int nchunk,
     T* __restrict__ D, T* __restrict__ Qout, int32_t* __restrict__ skip, T tol, int absmode,
@@ -473,19 +589,20 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   constexpr int NT = evd_threads(W);
   constexpr int NWAVE = NT / SVDJ_WAVE;
   constexpr int N = 2 * W;
-  constexpr int R = N - 1;              // steps per sweep
+  using O = Ord<W, ORD>;
+  constexpr int R = O::R;               // steps per sweep
   constexpr int NTRI = N * (N - 1) / 2;
   constexpr int GPW = SVDJ_WAVE / W;    // Q row groups per wave
   constexpr int NGRP = (NWAVE - 1) * GPW;  // Q row groups (waves 1..NWAVE-1)
   constexpr int RPL = (N + NGRP - 1) / NGRP;  // Q rows per lane (the last group may idle)
-  constexpr int MAXOFF = EvdDeal<W, NT>::MAXOFF;
+  constexpr int MAXOFF = EvdDeal<W, NT, ORD>::MAXOFF;
   static_assert(W >= 4 && W <= 64 && NWAVE >= 2, "EVD geometry");
 #ifdef SVDJ_EVD_Q32
   using QT = T;
 #else
   using QT = double;
 #endif
-  static constexpr EvdDeal<W, NT> deal{};
+  static constexpr EvdDeal<W, NT, ORD> deal{};
 
   __shared__ T Gb[2][NTRI + 1];  // off-diagonal G by position pair, double-buffered;
                                  // element NTRI takes the writes that go nowhere
@@ -525,7 +642,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     // store an entry at its step-0 position; fold it into the convergence
     // value and the "anything to rotate" test
     auto visit = [&](int r, int c, T g) {
-      Gb[0][tri_idx<N>(pos0<W>(r), pos0<W>(c))] = g;
+      Gb[0][tri_idx<N>(O::pos0(r), O::pos0(c))] = g;
       const T grr = dg[r], gcc = dg[c];
       const T d = sqrt(grr) * sqrt(gcc);
       if (d > T(0)) {
@@ -560,7 +677,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       // couplings inside a block are zero (blocks are kept internally orthogonal)
       for (int i = tid; i < N * N; i += NT) {
         const int r = i / N, c = i % N;
-        if (r < c && (c < W || r >= W)) Gb[0][tri_idx<N>(pos0<W>(r), pos0<W>(c))] = T(0);
+        if (r < c && (c < W || r >= W)) Gb[0][tri_idx<N>(O::pos0(r), O::pos0(c))] = T(0);
       }
       const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
       for (int gi = tid; gi < W * W / EV; gi += NT) {
@@ -618,18 +735,18 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       const int a = code >> 8, b = code & 255;
       ba[j] = a;
       bb[j] = b;
-      const int pa[2] = {slot_first_pos<W>(a), slot_second_pos<W>(a)};
-      const int pb[2] = {slot_first_pos<W>(b), slot_second_pos<W>(b)};
+      const int pa[2] = {O::first_pos(a), O::second_pos(a)};
+      const int pb[2] = {O::first_pos(b), O::second_pos(b)};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int x = pa[e >> 1], y = pb[e & 1];
         rd[j][e] = tri_idx<N>(x, y);
-        wr[j][e] = tri_idx<N>(pos_next<W>(x), pos_next<W>(y));
+        wr[j][e] = tri_idx<N>(O::pos_next(x), O::pos_next(y));
         if (j == 0 && tid < W) {
-          const int mt = next_meeting<W>(x, y);
+          const int mt = O::next_meeting(x, y);
           if (mt >= 0) {
             wr[j][e] = NTRI;  // a within-slot entry next step: written one phase later
-            pw = tri_idx<N>(pos_next<W>(pos_next<W>(x)), pos_next<W>(pos_next<W>(y)));
+            pw = tri_idx<N>(O::pos_next(O::pos_next(x)), O::pos_next(O::pos_next(y)));
             sv = 256 * e + mt;
           }
         }
@@ -642,8 +759,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   const bool qlane = wave > 0;
   const int slot = lane % W;
   const int grp = (wave - 1) * GPW + lane / W;
-  int pf = slot == 0 ? N - 1 : slot;          // first player of this slot
-  int ps = slot == 0 ? 0 : N - 1 - slot;      // second player
+  int pf = O::first0(slot);   // first player of this slot
+  int ps = O::second0(slot);  // second player
   QT qf[RPL], qs[RPL];
 #pragma unroll
   for (int i = 0; i < RPL; ++i) {
@@ -671,9 +788,9 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   // (OR-reduced over wave 0 once per sweep: no per-step flag store)
   int racc = 0, racc_next = 0;
   if (run && tid < W) {
-    const int fa = slot_first_pos<W>(tid), sa = slot_second_pos<W>(tid);
+    const int fa = O::first_pos(tid), sa = O::second_pos(tid);
     int p, q;
-    ring_slot<W>(tid, 0, p, q);
+    O::players(tid, 0, p, q);
     const T gpp = dg[p], gqq = dg[q];
     const T gpq = Gb[0][tri_idx<N>(fa, sa)];
     T c, s, t;
@@ -760,20 +877,10 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
           qf[i] = cq * x - sq * y;
           qs[i] = sq * x + cq * y;
         }
-        // advance the round robin: firsts shift right, seconds shift left
+        // advance the ordering (DPP lane moves of the slot layout)
 #pragma unroll
-        for (int i = 0; i < RPL; ++i) {
-          const QT f_r = dpp_shr1(qf[i]), s_r = dpp_shr1(qs[i]), s_l = dpp_shl1(qs[i]);
-          const QT nf = slot == 0 ? qf[i] : (slot == 1 ? s_r : f_r);
-          const QT ns = slot == W - 1 ? qf[i] : s_l;
-          qf[i] = nf;
-          qs[i] = ns;
-        }
-        const int f_r = dpp_shr1(pf), s_r = dpp_shr1(ps), s_l = dpp_shl1(ps);
-        const int nf = slot == 0 ? pf : (slot == 1 ? s_r : f_r);
-        const int ns = slot == W - 1 ? pf : s_l;
-        pf = nf;
-        ps = ns;
+        for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
+        O::move(pf, ps, slot);
         EVD_T(2);
         EVD_ACC(0, 0, 1);
         EVD_ACC(1, 1, 2);
@@ -810,7 +917,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     if (tid < W) {
       const int lb = (gs - 1) & 1;
       int p, q;
-      ring_slot<W>(tid, R - 1, p, q);
+      O::players(tid, R - 1, p, q);
       D[p < W ? bi * W + p : bj * W + (p - W)] = rdp[lb][tid];
       D[q < W ? bi * W + q : bj * W + (q - W)] = rdq[lb][tid];
     }
@@ -1199,7 +1306,8 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                            uint32_t* metric) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
-  const int full = c.modes ? c.modes[s] : 0;
+  const int mode = c.modes ? c.modes[s] : 0;  // 0 cross, 1 full Gram, 2 cross + bipartite EVD
+  const int full = mode == 1;
   constexpr int XS = gram_xsplit<T, W>();
   if (full) {
     if constexpr (XS > 1)  // see GRAM_SPLIT
@@ -1213,9 +1321,14 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   }
   SVDJ_LAUNCH_CHECK();
-  hipLaunchKernelGGL((evd_kernel<T, W>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr, full,
-                     c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode, max_inner,
-                     metric);
+  if (mode == 2)
+    hipLaunchKernelGGL((evd_kernel<T, W, EVD_BIP>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr,
+                       0, c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode,
+                       max_inner, metric);
+  else
+    hipLaunchKernelGGL((evd_kernel<T, W, EVD_CYCLIC>), dim3(c.P), dim3(evd_threads(W)), 0, c.st,
+                       pr, full, c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode,
+                       max_inner, metric);
   SVDJ_LAUNCH_CHECK();
   return 0;
 }
@@ -1447,7 +1560,8 @@ extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, 
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                 int ldv, void* D, int ncols, double tol, int tol_mode,
-                                int max_inner, int max_sweeps, void* ws, size_t ws_bytes,
+                                int max_inner, int max_sweeps, int inner_order, void* ws,
+                                size_t ws_bytes,
                                 uint32_t* metric, double* hist, int mma, void* stream) {
   if (W <= 0 || ncols % W) {
     set_error("ncols %d not a multiple of W %d", ncols, W);
@@ -1470,7 +1584,11 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
       o[2 * k + 1] = a < b ? b : a;
     }
   }
-  std::vector<int32_t> modes(steps, 0);
+  if (inner_order < 0 || inner_order > 1) {
+    set_error("inner_order %d (0 cyclic, 1 bipartite)", inner_order);
+    return -2;
+  }
+  std::vector<int32_t> modes(steps, inner_order ? 2 : 0);
   modes[0] = 1;
   hipStream_t st = (hipStream_t)stream;
   int32_t* dpairs = nullptr;

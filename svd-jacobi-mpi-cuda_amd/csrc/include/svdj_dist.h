@@ -52,6 +52,7 @@ typedef struct {
   int tol_mode;               // 0 relative, 1 absolute
   int max_sweeps;
   int mma;                    // matrix-core mode of the apply (svdj_block_steps)
+  int inner_order;            // EVD of the cross steps: 0 cyclic, 1 bipartite (mode 2)
   void* stream_a;             // two compute streams (distinct)
   void* stream_b;
   void* stream_comm;          // exchange stream, or NULL (created per call).  HIP maps

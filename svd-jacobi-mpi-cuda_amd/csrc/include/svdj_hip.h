@@ -58,7 +58,8 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   3. Apply (MFMA):  [A_bi A_bj] <- [A_bi A_bj] Q ,  [V_bi V_bj] <- .. Q
 // D (device, dtype, [ncols]) holds squared column norms; updated in place.
 //   pairs   device int32 [steps][P][2] block indices
-//   modes   host   int32 [steps] (0 cross / 1 full), NULL = all cross
+//   modes   host   int32 [steps] (0 cross / 1 full / 2 cross with the bipartite
+//           EVD ordering, W steps instead of 2W-1), NULL = all cross
 //   metric  device uint32[2] as for the scalar path.
 //   tol_mode 0: rotate when |g_pq| > tol sqrt(g_pp g_qq) (relative, default);
 //            1: when |g_pq| > tol (the reference's absolute TOLERANCE test).
@@ -87,10 +88,12 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
                       uint32_t* metric, int mma);
 
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
-// first step of every sweep in full mode.  Returns sweeps, <0 on error.
+// first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
+// step, 1 = bipartite EVD in the cross steps (mode 2).  Returns sweeps, <0 on
+// error.
 int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, int ncols, double tol, int tol_mode,
-                     int max_inner_sweeps, int max_sweeps, void* workspace,
+                     int max_inner_sweeps, int max_sweeps, int inner_order, void* workspace,
                      size_t ws_bytes, uint32_t* metric, double* hist,
                      int mma, void* stream);
 

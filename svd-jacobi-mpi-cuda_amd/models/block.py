@@ -60,7 +60,8 @@ class BlockJacobi(Solver):
         with Timer(device) as tm:
             D = K.col_norms2(At, m_pad)
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
-                                         cfg.max_sweeps, mma=mma, tol_mode=cfg.tol_mode)
+                                         cfg.max_sweeps, mma=mma, tol_mode=cfg.tol_mode,
+                                         inner_order=cfg.inner_order)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:n, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:n, :n].t() if want_v else None

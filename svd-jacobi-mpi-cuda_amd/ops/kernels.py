@@ -214,6 +214,19 @@ def block_workspace(dtype, W, P, m_pad, device, slot: int = 0, pool: dict | None
     return ws
 
 
+INNER_ORDERS = ("cyclic", "bipartite")
+
+
+def step_modes(modes, inner_order="cyclic"):
+    """Plan modes (0 cross, 1 full) -> kernel modes: with the bipartite inner
+    ordering cross steps become mode 2 (block.hip EVD_BIP, W EVD steps instead
+    of 2W-1); full steps always use the cyclic EVD."""
+    if inner_order not in INNER_ORDERS:
+        raise ValueError(f"inner_order must be one of {INNER_ORDERS}, got {inner_order!r}")
+    bip = inner_order == "bipartite"
+    return [2 if (bip and int(x) == 0) else int(x) for x in modes]
+
+
 def check_block(dtype, W):
     if W not in SUPPORTED_BLOCK.get(dtype, ()):
         raise ValueError(f"block width {W} unsupported for {dtype}; supported "
@@ -221,11 +234,13 @@ def check_block(dtype, W):
 
 
 def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0,
-                mma="native", pool: dict | None = None, tol_mode="relative"):
+                mma="native", pool: dict | None = None, tol_mode="relative",
+                inner_order="cyclic"):
     """Run ``len(modes)`` block steps on the current stream.  pairs: int32
     (steps, P, 2) on At's device (block indices local to At); modes: list of
-    0 (cross) / 1 (full).  Chains running concurrently on different streams
-    must use different ``ws_slot`` values."""
+    0 (cross) / 1 (full) (see step_modes for ``inner_order``).  Chains running
+    concurrently on different streams must use different ``ws_slot`` values."""
+    modes = step_modes(modes, inner_order)
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
     steps, P = int(pairs.shape[0]), int(pairs.shape[1])
@@ -243,14 +258,15 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             _stream(At)), "block_steps")
     else:
         for s in range(steps):
-            mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, bool(modes[s]), tol,
-                                      max_inner, tol_mode=tol_mode_code(tol_mode))
+            mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
+                                      max_inner, tol_mode=tol_mode_code(tol_mode),
+                                      order="bipartite" if modes[s] == 2 else "cyclic")
             metric[0] = max(float(metric[0]), mx)
             metric[1] += nrot
 
 
 def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native",
-                 pool: dict | None = None, tol_mode="relative"):
+                 pool: dict | None = None, tol_mode="relative", inner_order="cyclic"):
     """Two independent chains of block steps, staggered (svdj_block_steps2).
     ``chain_x = (pairs, modes, ws_slot, stream)``: device pairs (steps, P, 2),
     host modes, a workspace slot and the torch stream of that chain.  Step s
@@ -259,7 +275,7 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     if not At.is_cuda:
         for pairs, modes, slot, _ in (chain_a, chain_b):
             block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool,
-                        tol_mode)
+                        tol_mode, inner_order)
         return
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
@@ -267,7 +283,7 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     for pairs, modes, slot, stream in (chain_a, chain_b):
         steps, P = int(pairs.shape[0]), int(pairs.shape[1])
         ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool)
-        md = (C.c_int32 * max(steps, 1))(*[int(x) for x in modes])
+        md = (C.c_int32 * max(steps, 1))(*step_modes(modes, inner_order))
         args.append((_ptr(pairs), P, steps, md, _ptr(ws), ws.numel(),
                      C.c_void_p(stream.cuda_stream)))
     n_v = Vt.shape[1] if Vt is not None else 0
@@ -289,9 +305,11 @@ def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
 
 
 def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
-                tol_mode="relative"):
+                tol_mode="relative", inner_order="cyclic"):
     """Single-device block Jacobi (round-robin over ncols/W blocks, first
-    step of each sweep full).  Returns (sweeps, hist)."""
+    step of each sweep full; cross steps with ``inner_order``).  Returns
+    (sweeps, hist)."""
+    step_modes([], inner_order)  # validates
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
     ncols = At.shape[0]
@@ -305,7 +323,8 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
         sweeps = hip_check(hip_lib().svdj_block_solve(
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
             ncols, float(tol), tol_mode_code(tol_mode), int(max_inner), int(max_sweeps),
-            _ptr(ws), ws.numel(), _ptr(metric), hist, mma_code(mma, At.dtype), _stream(At)),
+            INNER_ORDERS.index(inner_order), _ptr(ws), ws.numel(), _ptr(metric), hist,
+            mma_code(mma, At.dtype), _stream(At)),
             "block_solve")
         return sweeps, [hist[i] for i in range(sweeps)]
     from ..parallel.schedule import round_robin
@@ -317,7 +336,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
     for _ in range(max_sweeps):
         metric = new_metric("cpu")
         block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric,
-                    tol_mode=tol_mode)
+                    tol_mode=tol_mode, inner_order=inner_order)
         mx, nrot = read_metric(metric)
         hist.append(mx)
         if nrot == 0:
@@ -326,7 +345,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
 
 
 __all__ = [
-    "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "dtype_code", "new_metric", "reset_metric",
+    "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",

@@ -77,20 +77,31 @@ def round_robin_pairs(N):
 _RR_CACHE = {}
 
 
-def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0):
+def bipartite_pairs(W):
+    """Cross-pair ordering of the bipartite EVD (block.hip Ord<W, EVD_BIP>):
+    step t pairs local column a of block i with column (a + t) mod W of
+    block j (player W + ...), W steps per sweep."""
+    return [[(a, W + (a + t) % W) for a in range(W)] for t in range(W)]
+
+
+def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
     """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
 
-    Same round-robin ordering, threshold and update formulas as the LDS
-    kernel (csrc/hip/block.hip evd_kernel).  Returns (G_diag_final, Q, rotated).
+    Same orderings (``cyclic``: circle-method round robin over all pairs;
+    ``bipartite``: the cross pairs only), threshold and update formulas as
+    the LDS kernel (csrc/hip/block.hip evd_kernel).  Returns (G_diag_final,
+    Q, rotated).
     """
     G = G.clone()
     P, N, _ = G.shape
     Q = torch.eye(N, dtype=G.dtype).expand(P, N, N).clone()
-    sched = _RR_CACHE.get(N)
+    key = (N, order)
+    sched = _RR_CACHE.get(key)
     if sched is None:
+        prs_all = round_robin_pairs(N) if order == "cyclic" else bipartite_pairs(N // 2)
         sched = [(torch.tensor([a for a, b in prs]), torch.tensor([b for a, b in prs]))
-                 for prs in round_robin_pairs(N)]
-        _RR_CACHE[N] = sched
+                 for prs in prs_all]
+        _RR_CACHE[key] = sched
     rotated = torch.zeros(P, dtype=torch.bool)
     for _ in range(max_sweeps):
         sweep_rot = torch.zeros(P, dtype=torch.bool)
@@ -125,11 +136,13 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0):
     return torch.diagonal(G, dim1=1, dim2=2).clone(), Q, rotated
 
 
-def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0):
+def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
+               order: str = "cyclic"):
     """One block step on P disjoint block pairs (pairs: (P, 2) block ids).
 
     Mirrors csrc/hip/block.hip (gram -> evd -> apply).  Updates At, Vt, D in
-    place.  Returns (maxconv, pairs_rotated).
+    place.  ``order`` is the EVD ordering of a cross step (a full step is
+    always cyclic).  Returns (maxconv, pairs_rotated).
     """
     P = pairs.shape[0]
     if P == 0:
@@ -156,7 +169,8 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0):
     den = dg[:, :, None] * dg[:, None, :]
     R = torch.where(den > 0, G.abs() / torch.where(den > 0, den, torch.ones_like(den)), torch.zeros_like(den))
     maxconv = float(R[:, mask].max()) if mask.any() else 0.0
-    lam, Q, rotated = jacobi_evd(G, tol, max_inner, tol_mode)
+    lam, Q, rotated = jacobi_evd(G, tol, max_inner, tol_mode,
+                                 order="cyclic" if full else order)
     if bool(rotated.any()):
         sel = rotated
         Qs = Q[sel]

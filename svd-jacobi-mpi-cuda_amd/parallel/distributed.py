@@ -281,11 +281,13 @@ class DistributedBlockJacobi(Solver):
 
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
-                              metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode)
+                              metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
+                              inner_order=cfg.inner_order)
 
             def run_pair(a, b):
                 K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
-                               mma=mma, pool=self._ws, tol_mode=cfg.tol_mode)
+                               mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
+                               inner_order=cfg.inner_order)
 
             if not cfg.stagger:
                 run_pair = None
@@ -305,7 +307,7 @@ class DistributedBlockJacobi(Solver):
                     with trace_range(f"svdj.round{r}"):
                         K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
                                       cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
-                                      tol_mode=cfg.tol_mode)
+                                      tol_mode=cfg.tol_mode, inner_order=cfg.inner_order)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1

@@ -127,3 +127,17 @@ def test_cholqr2_matches_householder():
         pre.qr(B, torch.float64, method="cholqr2")
     Q2, R2 = pre.qr(B, torch.float64, method="householder")
     torch.testing.assert_close(Q2 @ R2, B, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("order", ["cyclic", "bipartite"])
+def test_block_inner_order_cpu(order):
+    """Block path on CPU (reference kernels) with both EVD orderings of the
+    cross steps: converges to the same SVD, sweep counts within one or two."""
+    A = svdj.utils.inputs.random_dense(200, 128, seed=21)
+    res = svdj.svd(A, method="block", dtype=torch.float64,
+                   inner_order=order, precondition="none")
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-12 and rep["orth_v_fro"] < 1e-11, rep
+    with pytest.raises(ValueError):
+        svdj.svd(A, method="block", inner_order="sideways")

@@ -270,3 +270,53 @@ def test_fp64_block_widths_end_to_end(svdj, cuda, W):
     rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
     assert rep["residual_rel"] < 5e-12 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
     assert rep["orth_u_fro"] < 5e-11 and rep["orth_v_fro"] < 5e-11, rep
+
+
+@pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64),
+                                     (torch.float64, 32), (torch.float64, 64)])
+def test_block_step_bipartite_matches_reference(svdj, cuda, dtype, W):
+    """Cross step with the bipartite EVD ordering (mode 2, block.hip
+    Ord<W, EVD_BIP>: W steps of the cross pairs, DPP rotate + permlane32 swap
+    of the register Q) against the fp64 reference with the same ordering:
+    same rotation count, D and rotated panels to rounding level."""
+    K = svdj.ops.kernels
+    R = svdj.ops.reference
+    nb = 4
+    n, m, m_pad = nb * W, 500, 512
+    A64 = _rand_At(n, m_pad, m, torch.float64, "cpu", seed=7)
+    for b in range(nb):  # cross steps start from internally orthogonal blocks
+        q, _ = torch.linalg.qr(A64[b * W:(b + 1) * W, :m].t())
+        A64[b * W:(b + 1) * W, :m] = (q * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+    At = A64.to(dtype).to(cuda)
+    Vt = torch.zeros(n, 256, dtype=dtype, device=cuda)
+    K.set_identity(Vt, n)
+    D = K.col_norms2(At, m_pad)
+    pairs = torch.tensor([[[0, 3], [1, 2]]], dtype=torch.int32)
+    At64, Vt64, D64 = At.double().cpu(), Vt.double().cpu(), D.double().cpu()
+    tol = 1e-6 if dtype == torch.float32 else 1e-13
+    metric = K.new_metric(cuda)
+    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [0], tol, 1, metric,
+                  inner_order="bipartite")
+    mx_ref, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, False, tol, 1,
+                                    order="bipartite")
+    mx, nrot = K.read_metric(metric)
+    assert nrot == nrot_ref == 2
+    assert math.isclose(mx, mx_ref, rel_tol=1e-3)
+    rt = 3e-5 if dtype == torch.float32 else 1e-11
+    torch.testing.assert_close(At.double().cpu()[:, :m], At64[:, :m], rtol=rt, atol=rt)
+    torch.testing.assert_close(Vt.double().cpu()[:, :n], Vt64[:, :n], rtol=rt, atol=rt)
+    torch.testing.assert_close(D.double().cpu(), D64, rtol=rt, atol=rt)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_svd_end_to_end_bipartite(svdj, cuda, dtype):
+    """Whole solve with bipartite cross steps: same accuracy bounds as the
+    cyclic inner ordering."""
+    m, n = 520, 384
+    A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=3)
+    res = svdj.svd(A.to(cuda), method="block", dtype=dtype, inner_order="bipartite")
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
+    r, sg, ou, ov = _E2E_BOUNDS[("block", dtype, "native")]
+    assert rep["residual_rel"] < r and rep["sigma_max_abs_err_over_smax"] < sg, rep
+    assert rep["orth_u_fro"] < ou and rep["orth_v_fro"] < ov, rep

@@ -317,3 +317,144 @@ def test_evd_position_space_emulation(W):
     for a in range(W):
         p, q = _ring_slot(W, a, R - 1)
         np.testing.assert_allclose([rec[lb][a][2], rec[lb][a][3]], [G[p, p], G[q, q]], rtol=1e-12)
+
+
+# ---- bipartite inner ordering (cross steps): X players fixed at positions
+# 0..W-1, the Y player at Y-position p (position W+p) moves to p-1 (mod W)
+# every step; slot a pairs positions (a, W+a).  Python twins of block.hip
+# BipOrder, and the same position-space emulation as above.
+def _bip_players(W, a, st):
+    return a, W + (a + st) % W
+
+
+def _bip_pos_next(W, P):
+    return P if P < W else W + (P - W - 1) % W
+
+
+def _bip_next_meeting(W, P1, P2):
+    n1, n2 = _bip_pos_next(W, P1), _bip_pos_next(W, P2)
+    if (n1 < W) == (n2 < W):
+        return -1
+    s1, s2 = n1 % W, n2 % W
+    if s1 != s2:
+        return -1
+    return 2 * s1 + (1 if n1 < W else 0)
+
+
+@pytest.mark.parametrize("W", [3, 4, 8, 32, 64])
+def test_bip_next_step_pairs_are_static(W):
+    """Bipartite ordering: every cross pair once per W steps, and the coupling
+    of each next-step pair sits in exactly one slot-pair block (at most one per
+    block), at a static position."""
+    seen = set()
+    for st in range(W):
+        nxt = {}
+        for a in range(W):
+            p, q = _bip_players(W, a, st)
+            seen.add((p, q))
+            p1, q1 = _bip_players(W, a, (st + 1) % W)
+            nxt[frozenset((p1, q1))] = (a, p1)
+        found = 0
+        for a in range(W):
+            for b in range(a + 1, W):
+                per_block = 0
+                pa, pb = [a, W + a], [b, W + b]
+                P, Q = _bip_players(W, a, st), _bip_players(W, b, st)
+                for e in range(4):
+                    x, y = P[e >> 1], Q[e & 1]
+                    mt = _bip_next_meeting(W, pa[e >> 1], pb[e & 1])
+                    if frozenset((x, y)) in nxt:
+                        sl, first = nxt[frozenset((x, y))]
+                        assert mt == 2 * sl + (1 if first == x else 0)
+                        found += 1
+                        per_block += 1
+                    else:
+                        assert mt == -1
+                assert per_block <= 1
+        assert found == W
+    assert len(seen) == W * W
+
+
+@pytest.mark.parametrize("W", [3, 4, 8])
+def test_bip_position_space_emulation(W):
+    """The kernel's position-space data flow with the bipartite ordering
+    against a plain player-space Jacobi over the cross pairs: same rotations,
+    same final diagonal."""
+    N, R = 2 * W, W
+    rng = np.random.default_rng(W + 100)
+    X = rng.random((3 * N, N))
+    G0 = X.T @ X
+    tol = 1e-14
+    G = G0.copy()
+    ref_rots = []
+    for st in range(R):
+        rots = []
+        for a in range(W):
+            p, q = _bip_players(W, a, st)
+            c, s, t, _ = _rot(G[p, p], G[q, q], G[p, q], tol)
+            rots.append((c, s))
+            J = np.eye(N)
+            J[p, p], J[p, q], J[q, p], J[q, q] = c, s, -s, c
+            dpp, dqq, gpq = G[p, p], G[q, q], G[p, q]
+            G = J.T @ G @ J
+            if t != 0.0:
+                G[p, p], G[q, q] = dpp - t * gpq, dqq + t * gpq
+                G[p, q] = G[q, p] = 0.0
+        ref_rots.append(rots)
+    nxt = lambda P: _bip_pos_next(W, P)  # noqa: E731
+    Gb = [np.zeros(N * (N - 1) // 2), np.zeros(N * (N - 1) // 2)]
+    for r in range(N):
+        for c in range(r + 1, N):
+            Gb[0][_tri(N, r, c)] = G0[r, c]  # pos0 is the identity
+    rec = [dict(), dict()]
+    for a in range(W):
+        fa, sa = a, W + a
+        g = Gb[0][_tri(N, fa, sa)]
+        c, s, t, rot = _rot(G0[fa, fa], G0[sa, sa], g, tol)
+        dp, dq = (G0[fa, fa] - t * g, G0[sa, sa] + t * g) if rot else (G0[fa, fa], G0[sa, sa])
+        Gb[1][_tri(N, nxt(fa), nxt(sa))] = 0.0 if rot else g
+        rec[0][a] = (c, s, dp, dq)
+    blocks = []
+    for a in range(W):
+        for b in range(a + 1, W):
+            pa, pb = [a, W + a], [b, W + b]
+            duty = []
+            for e in range(4):
+                mt = _bip_next_meeting(W, pa[e >> 1], pb[e & 1])
+                if mt >= 0:
+                    x, y = pa[e >> 1], pb[e & 1]
+                    duty.append((e, mt, _tri(N, nxt(nxt(x)), nxt(nxt(y)))))
+            blocks.append((a, b, pa, pb, duty, [0.0]))
+    emu_rots = [[rec[0][a][:2] for a in range(W)]]
+    for gs in range(R):
+        b, nb = gs & 1, (gs & 1) ^ 1
+        for (a, bb, pa, pb, duty, pend) in blocks:
+            if gs > 0:
+                for k, (_, _, addr) in enumerate(duty):
+                    Gb[nb][addr] = pend[k]
+            g = [Gb[b][_tri(N, pa[e >> 1], pb[e & 1])] for e in range(4)]
+            ca, sa = rec[b][a][:2]
+            cb, sb = rec[b][bb][:2]
+            h00, h01 = ca * g[0] - sa * g[2], ca * g[1] - sa * g[3]
+            h10, h11 = sa * g[0] + ca * g[2], sa * g[1] + ca * g[3]
+            h = [cb * h00 - sb * h01, sb * h00 + cb * h01, cb * h10 - sb * h11, sb * h10 + cb * h11]
+            solved = set()
+            for k, (e, mt, _) in enumerate(duty):
+                ns, xf = mt >> 1, mt & 1
+                dx = rec[b][a][3] if e >> 1 else rec[b][a][2]
+                dy = rec[b][bb][3] if e & 1 else rec[b][bb][2]
+                df, ds = (dx, dy) if xf else (dy, dx)
+                c, s, t, rot = _rot(df, ds, h[e], tol)
+                rec[nb][ns] = (c, s, df - t * h[e], ds + t * h[e]) if rot else (c, s, df, ds)
+                pend[k] = 0.0 if rot else h[e]
+                solved.add(e)
+            for e in range(4):
+                if e not in solved:
+                    Gb[nb][_tri(N, nxt(pa[e >> 1]), nxt(pb[e & 1]))] = h[e]
+        if gs + 1 < R:
+            emu_rots.append([rec[nb][a][:2] for a in range(W)])
+    np.testing.assert_allclose(np.array(emu_rots), np.array(ref_rots), rtol=1e-12, atol=1e-14)
+    lb = (R - 1) & 1
+    for a in range(W):
+        p, q = _bip_players(W, a, R - 1)
+        np.testing.assert_allclose([rec[lb][a][2], rec[lb][a][3]], [G[p, p], G[q, q]], rtol=1e-12)
