@@ -50,7 +50,7 @@ class SolverConfig:
     tol_mode: str = "relative"      # relative | absolute (reference parity)
     max_sweeps: int = 60            # reference: 1 (main.cu:482)
     max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)
-    inner_order: str = "cyclic"     # block path, cross steps: cyclic (2W-1 EVD steps, all
+    inner_order: str = "bipartite"  # block path, cross steps: cyclic (2W-1 EVD steps, all
                                     # pairs) | bipartite (W steps, cross pairs only)
     ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)

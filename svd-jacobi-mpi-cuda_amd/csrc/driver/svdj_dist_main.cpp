@@ -45,7 +45,7 @@
 namespace {
 
 struct Opts {
-  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 0;
+  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
   bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;

@@ -144,7 +144,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s N [--m M] [--input triu|dense] [--dtype f32|f64] ...\n", argv[0]);
     return 1;
   }
-  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60, inner_order = 0;
+  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60, inner_order = 1;
   unsigned seed = 1000000;
   double tol = -1;
   bool verify = false;

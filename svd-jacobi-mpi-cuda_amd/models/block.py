@@ -19,19 +19,22 @@ from .base import SVDResult, Solver, Timer
 def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     """Block width W for ``n`` columns per GPU of ``m`` rows.
 
-    W=64 halves the steps and the per-byte traffic of the Gram and the apply
-    but its EVD is ~4x slower (190 vs 45 us), and it halves the number of
-    pairs a step can run at once.  It pays when the rows are long (the
-    apply / Gram dominate) and there are still >= 16 pairs per half task.
-    Measured on MI355X (profiles/r2_configs, profiles/r2_simgrid):
-      * 1 GPU n x n, s per solve W=32 / W=64: fp32 8192: 1.23 / 1.31,
-        16384: 9.07 / 6.81; fp64 8192: 2.50 / 2.92, 16384: 17.8 / 16.5.
-      * rank plan of the 16384^2 fp32 job, ms per sweep W=32 / W=64: P=2
-        (8192 columns per GPU): 354 / 244, P=4 (4096): 187 / 155, P=8 (2048):
-        93 / 115.
+    W=64 halves the steps and the per-byte traffic of the Gram and the apply,
+    but its EVD is slower and a step holds half as many pairs.  It pays when
+    the rows are long (the Gram and apply dominate) and a half task still
+    has enough pairs.  Measured on MI355X with the bipartite cross-step EVD
+    (profiles/r2_simgrid2), time per solve or per sweep, W=32 / W=64:
+      * fp32, 1 GPU n x n: 4096 0.179 / 0.186 s, 8192 1.13 / 0.88 s,
+        12288 3.92 / 2.63 s;
+      * fp32 rank plans, ms per sweep: 16384^2 on P=2 345 / 216, P=4
+        159 / 125, P=8 (2048 columns per GPU) 83 / 69; 8192^2 on P=8 (1024
+        columns) 22.2 / 26.2; 65536^2 on P=8 4268 / 1787;
+      * fp64, 1 GPU: 5000 0.54 / 0.80 s, 8192 2.47 / 2.56 s, 16384 17.8 /
+        16.5 s (the fp64 W=64 EVD keeps a 2x larger G in LDS).
     """
-    del dtype  # same crossover for fp32 and fp64 (see the measurements above)
-    return 64 if (m >= 12288 and n >= 4096) else 32
+    if dtype == torch.float64:
+        return 64 if (m >= 12288 and n >= 4096) else 32
+    return 64 if (m >= 8192 and n >= 2048) else 32
 
 
 class BlockJacobi(Solver):
