@@ -4,7 +4,7 @@
 // (tools/svd_jacobi.py under torchrun) -- one process per GPU.
 //
 //   svdj_main N [--m M] [--input triu|dense] [--seed S] [--dtype f32|f64]
-//               [--method block|scalar] [--block W] [--max-sweeps K]
+//               [--method block|scalar] [--block W (default: by size)] [--max-sweeps K]
 //               [--tol T] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite]
 //               [--verify] [--report-dir DIR]
 //
@@ -144,7 +144,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s N [--m M] [--input triu|dense] [--dtype f32|f64] ...\n", argv[0]);
     return 1;
   }
-  int n = std::atoi(argv[1]), m = n, W = 32, max_sweeps = 60, inner_order = 1;
+  int n = std::atoi(argv[1]), m = n, W = 0, max_sweeps = 60, inner_order = 1;
   unsigned seed = 1000000;
   double tol = -1;
   bool verify = false;
@@ -178,6 +178,8 @@ int main(int argc, char** argv) {
   else
     svdj_ref_triu_input(m, n, A.data(), m, seed);
   const int mma_code = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
+  if (W == 0)  // models/block.py choose_block
+    W = dtype == "f32" ? ((m >= 8192 && n >= 2048) ? 64 : 32) : ((m >= 12288 && n >= 4096) ? 64 : 32);
   if (dtype == "f32")
     return run<float>(m, n, A, method, W, max_sweeps, tol, mma_code, inner_order, verify, report_dir);
   return run<double>(m, n, A, method, W, max_sweeps, tol, 0, inner_order, verify, report_dir);
