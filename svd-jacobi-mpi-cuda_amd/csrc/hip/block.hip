@@ -1223,10 +1223,20 @@ struct Geometry {
   int a_chunks, rows_a, v_chunks, rows_v;
 };
 
-static Geometry make_geometry(int P, int m_pad, int n_v) {
+static Geometry make_geometry(int W, int P, int m_pad, int n_v) {
   Geometry g;
-  // Gram: aim for >= 2 waves of workgroups over 256 CUs, >= 128 rows/chunk.
-  int want = (512 + P - 1) / P;
+  // Gram: split-K over row chunks (>= 128 rows each), ~1024 workgroups for
+  // W=32 and ~512 for W=64.  Few pairs per step (many GPUs) want many chunks
+  // (the Gram is latency-bound there: 16384^2 8-GPU rank plan, W=32, 80.9 ->
+  // 67.0 ms per sweep going from 512 to 1024); many pairs want few (every
+  // chunk is a slab the EVD sums: 1-GPU 16384^2, W=64, 5.92 s at 512 vs
+  // 6.23 s at 2048), and W=64 slabs are 4x larger.
+  static const int gram_env = [] {
+    const char* e = getenv("SVDJ_GRAM_WG_TARGET");  // tuning experiments only
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+  }();
+  const int gram_target = gram_env ? gram_env : (W == 32 ? 1024 : 512);
+  int want = (gram_target + P - 1) / P;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.grows = round_up((m_pad + g.gchunks - 1) / g.gchunks, 128);
@@ -1248,7 +1258,7 @@ static Geometry make_geometry(int P, int m_pad, int n_v) {
 }
 
 static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
-  Geometry g = make_geometry(P, m_pad, 0);
+  Geometry g = make_geometry(W, P, m_pad, 0);
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
@@ -1285,7 +1295,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   }
   c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
   c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
-  c.g = make_geometry(P, m_pad, V ? n_v : 0);
+  c.g = make_geometry(W, P, m_pad, V ? n_v : 0);
   char* w = (char*)ws;
   c.slabs = (T*)w;
   w += ((size_t)P * c.g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
