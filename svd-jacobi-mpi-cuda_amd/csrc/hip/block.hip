@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 namespace svdj {
@@ -723,8 +724,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 
   // ---- this thread's blocks and their static addresses
   int ba[MAXOFF], bb[MAXOFF];
-  int rd[MAXOFF][4], wr[MAXOFF][4];  // read / write element index (NTRI: no write)
-  int pw = NTRI, sv = -1;  // solve duty (256*e + meeting; j = 0 only) and its pending address
+  int rd[MAXOFF][4], wr[MAXOFF][4];  // read / write BYTE offsets into a G buffer (NTRI: no write)
+  int pw = (int)sizeof(T) * NTRI, sv = -1;  // solve duty (256*e + meeting; j = 0 only), pending byte offset
 #pragma unroll
   for (int j = 0; j < MAXOFF; ++j) {
     const int code = deal.blk[j * NT + tid];
@@ -740,13 +741,13 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int x = pa[e >> 1], y = pb[e & 1];
-        rd[j][e] = tri_idx<N>(x, y);
-        wr[j][e] = tri_idx<N>(O::pos_next(x), O::pos_next(y));
+        rd[j][e] = (int)sizeof(T) * tri_idx<N>(x, y);
+        wr[j][e] = (int)sizeof(T) * tri_idx<N>(O::pos_next(x), O::pos_next(y));
         if (j == 0 && tid < W) {
           const int mt = O::next_meeting(x, y);
           if (mt >= 0) {
-            wr[j][e] = NTRI;  // a within-slot entry next step: written one phase later
-            pw = tri_idx<N>(O::pos_next(O::pos_next(x)), O::pos_next(O::pos_next(y)));
+            wr[j][e] = (int)sizeof(T) * NTRI;  // within-slot entry next step: written one phase later
+            pw = (int)sizeof(T) * tri_idx<N>(O::pos_next(O::pos_next(x)), O::pos_next(O::pos_next(y)));
             sv = 256 * e + mt;
           }
         }
@@ -807,30 +808,47 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 
   // One block's update J^T G J (entries moved to their next-step positions)
   // and, for a duty block, the next step's rotation of its slot.
-  auto update_block = [&](int j, int b, int nb, bool duty, bool last) {
-    const T* __restrict__ Gr = Gb[b];
-    T* __restrict__ Gw = Gb[nb];
-    // the coupling of this step's pair, solved last phase (or in the
-    // prologue), moved on to its next-step position (dummy if no duty)
-    if (j == 0) Gw[pw] = pend;
-    // every LDS read of the block up front (static addresses)
-    const T g00 = Gr[rd[j][0]], g01 = Gr[rd[j][1]], g10 = Gr[rd[j][2]], g11 = Gr[rd[j][3]];
-    const T ca = rc[b][ba[j]], sa = rs[b][ba[j]], cb = rc[b][bb[j]], sb = rs[b][bb[j]];
-    T dx = T(0), dy = T(0);
-    const int e = sv >> 8;
+  // One block's update J^T G J (entries moved to their next-step positions)
+  // and, for a duty block, the next step's rotation of its slot.  Split in a
+  // read half and a compute/write half so a thread issues the LDS reads of
+  // ALL its blocks before any write: Gb[b] and Gb[nb] are disjoint but the
+  // compiler cannot prove it, so a fused per-block read-compute-write
+  // serialises the read latency of every block.
+  // G entry at byte offset `off` of buffer b (b is a compile-time constant in
+  // the unrolled step loop, so the buffer base folds into the ds offset)
+  auto gat = [&](int b, int off) -> T& {
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(&Gb[b][0]) + off);
+  };
+  struct BlkIn {
+    T g00, g01, g10, g11, ca, sa, cb, sb, dx, dy;
+  };
+  auto load_block = [&](int j, int b, bool duty, BlkIn& k) {
+    k.g00 = gat(b, rd[j][0]);
+    k.g01 = gat(b, rd[j][1]);
+    k.g10 = gat(b, rd[j][2]);
+    k.g11 = gat(b, rd[j][3]);
+    k.ca = rc[b][ba[j]];
+    k.sa = rs[b][ba[j]];
+    k.cb = rc[b][bb[j]];
+    k.sb = rs[b][bb[j]];
+    k.dx = k.dy = T(0);
     if (duty) {
-      dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
-      dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
+      const int e = sv >> 8;
+      k.dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
+      k.dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
     }
-    const T h00 = ca * g00 - sa * g10, h01 = ca * g01 - sa * g11;
-    const T h10 = sa * g00 + ca * g10, h11 = sa * g01 + ca * g11;
-    const T h[4] = {cb * h00 - sb * h01, sb * h00 + cb * h01, cb * h10 - sb * h11,
-                    sb * h10 + cb * h11};
+  };
+  auto finish_block = [&](int j, int nb, bool duty, bool last, const BlkIn& k) {
+    const T h00 = k.ca * k.g00 - k.sa * k.g10, h01 = k.ca * k.g01 - k.sa * k.g11;
+    const T h10 = k.sa * k.g00 + k.ca * k.g10, h11 = k.sa * k.g01 + k.ca * k.g11;
+    const T h[4] = {k.cb * h00 - k.sb * h01, k.sb * h00 + k.cb * h01, k.cb * h10 - k.sb * h11,
+                    k.sb * h10 + k.cb * h11};
     if (duty) {
+      const int e = sv >> 8;
       const int ns = (sv & 255) >> 1;
       const bool x_first = sv & 1;
       const T g = e == 0 ? h[0] : e == 1 ? h[1] : e == 2 ? h[2] : h[3];
-      const T df = x_first ? dx : dy, ds = x_first ? dy : dx;
+      const T df = x_first ? k.dx : k.dy, ds = x_first ? k.dy : k.dx;
       T c, sn, t;
       const bool rot = rotation_fast(df, ds, g, tol, absmode, c, sn, t);
       if (last) racc_next |= rot; else racc |= rot;
@@ -838,60 +856,77 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       publish(nb, ns, c, sn, t, df - t * g, ds + t * g);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Gw[wr[j][q]] = h[q];
+    for (int q = 0; q < 4; ++q) gat(nb, wr[j][q]) = h[q];
+  };
+  auto update_blocks = [&](int b, int nb, bool solver, bool last) {
+    BlkIn k[MAXOFF];
+#pragma unroll
+    for (int j = 0; j < MAXOFF; ++j)
+      if (ba[j] >= 0) load_block(j, b, solver && j == 0 && sv >= 0, k[j]);
+    // the coupling of this step's pair, solved last phase (or in the
+    // prologue), moved on to its next-step position (dummy if no duty)
+    gat(nb, pw) = pend;
+#pragma unroll
+    for (int j = 0; j < MAXOFF; ++j)
+      if (ba[j] >= 0) finish_block(j, nb, solver && j == 0 && sv >= 0, last, k[j]);
   };
 
   bool any = false;
   int gs = 0;  // global step counter: step gs reads buffer gs & 1, records gs & 1
-  for (int sw = 0; sw < (run ? max_inner : 0); ++sw) {
-    for (int st = 0; st < R; ++st, ++gs) {
-      EVD_T(0);
-      const int b = gs & 1, nb = b ^ 1;
-      const bool last = st + 1 == R;  // this phase solves step 0 of the next sweep
-      if (wave == 0) {
-        // solver wave: its duty blocks (lanes < W, j = 0) and nothing else of Q
-#pragma unroll
-        for (int j = 0; j < MAXOFF; ++j)
-          if (ba[j] >= 0) update_block(j, b, nb, j == 0 && sv >= 0, last);
-        if (last) {  // every rotation of sweep sw is decided by now
-          const int rot = __any(racc) ? 1 : 0;
-          if (lane == 0) rot_flag[sw & 1] = rot;
-          racc = racc_next;
-          racc_next = 0;
-        }
-        EVD_T(1);
-        EVD_T(2);
-        EVD_ACC(1, 1, 2);
-        EVD_ACC(0, 0, 1);
-      } else {
-        // Q waves: this step's Q rotation (records read up front)
-        const QT cq = rcq[b][slot], sq = rsq[b][slot];
-#pragma unroll
-        for (int j = 0; j < MAXOFF; ++j)
-          if (ba[j] >= 0) update_block(j, b, nb, false, last);
-        EVD_T(1);
-        // Q <- Q J in registers (c = 1, s = 0 for no rotation)
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) {
-          const QT x = qf[i], y = qs[i];
-          qf[i] = cq * x - sq * y;
-          qs[i] = sq * x + cq * y;
-        }
-        // advance the ordering (DPP lane moves of the slot layout)
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
-        O::move(pf, ps, slot);
-        EVD_T(2);
-        EVD_ACC(0, 0, 1);
-        EVD_ACC(1, 1, 2);
+  int sw = 0, st = 0;
+  // One step with the buffer parity as a compile-time constant (the loop
+  // below alternates the two instantiations): every G / record address is a
+  // loop-invariant register plus an immediate.  Returns true when done.
+  auto step = [&](auto parity) -> bool {
+    constexpr int b = decltype(parity)::value, nb = b ^ 1;
+    EVD_T(0);
+    const bool last = st + 1 == R;  // this phase solves step 0 of the next sweep
+    if (wave == 0) {
+      // solver wave: its duty blocks (lanes < W, j = 0) and nothing else of Q
+      update_blocks(b, nb, true, last);
+      if (last) {  // every rotation of sweep sw is decided by now
+        const int rot = __any(racc) ? 1 : 0;
+        if (lane == 0) rot_flag[sw & 1] = rot;
+        racc = racc_next;
+        racc_next = 0;
       }
-      __syncthreads();
-      EVD_T(3);
-      EVD_ACC(2, 0, 3);
+      EVD_T(1);
+      EVD_T(2);
+      EVD_ACC(1, 1, 2);
+      EVD_ACC(0, 0, 1);
+    } else {
+      // Q waves: this step's Q rotation (records read up front)
+      const QT cq = rcq[b][slot], sq = rsq[b][slot];
+      update_blocks(b, nb, false, last);
+      EVD_T(1);
+      // Q <- Q J in registers (c = 1, s = 0 for no rotation)
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) {
+        const QT x = qf[i], y = qs[i];
+        qf[i] = cq * x - sq * y;
+        qs[i] = sq * x + cq * y;
+      }
+      // advance the ordering (DPP lane moves of the slot layout)
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
+      O::move(pf, ps, slot);
+      EVD_T(2);
+      EVD_ACC(0, 0, 1);
+      EVD_ACC(1, 1, 2);
     }
-    if (!rot_flag[sw & 1]) break;
+    __syncthreads();
+    EVD_T(3);
+    EVD_ACC(2, 0, 3);
+    ++gs;
+    if (++st < R) return false;
+    st = 0;
+    if (!rot_flag[sw & 1]) return true;
     any = true;
-  }
+    return ++sw >= max_inner;
+  };
+  if (run && max_inner > 0)
+    while (!step(std::integral_constant<int, 0>{}) && !step(std::integral_constant<int, 1>{})) {
+    }
   EVD_T(7);
   EVD_ACC(5, 8, 7);
 
@@ -1225,17 +1260,18 @@ struct Geometry {
 
 static Geometry make_geometry(int W, int P, int m_pad, int n_v) {
   Geometry g;
-  // Gram: split-K over row chunks (>= 128 rows each), ~1024 workgroups for
-  // W=32 and ~512 for W=64.  Few pairs per step (many GPUs) want many chunks
-  // (the Gram is latency-bound there: 16384^2 8-GPU rank plan, W=32, 80.9 ->
-  // 67.0 ms per sweep going from 512 to 1024); many pairs want few (every
-  // chunk is a slab the EVD sums: 1-GPU 16384^2, W=64, 5.92 s at 512 vs
-  // 6.23 s at 2048), and W=64 slabs are 4x larger.
+  // Gram: split-K over row chunks (>= 128 rows each), ~512 workgroups.
+  // Many pairs per step want few chunks (every chunk is a slab the EVD sums:
+  // 1-GPU 16384^2, W=64, 5.92 s at 512 vs 6.23 s at 2048).  With few pairs
+  // (many GPUs) the two chains' phase relation makes the optimum jump between
+  // 512 and 1024 from one kernel revision to the next (8-GPU rank plan,
+  // W=32: 80.9 / 67.0 ms per sweep before the EVD step unroll, 62 / 81 after;
+  // profiles/r2_stagger).
   static const int gram_env = [] {
     const char* e = getenv("SVDJ_GRAM_WG_TARGET");  // tuning experiments only
     return e && atoi(e) > 0 ? atoi(e) : 0;
   }();
-  const int gram_target = gram_env ? gram_env : (W == 32 ? 1024 : 512);
+  const int gram_target = gram_env ? gram_env : 512;
   int want = (gram_target + P - 1) / P;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
@@ -1443,17 +1479,35 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
     set_error("stagger events unavailable");
     return -100;
   }
+  // SVDJ_STAGGER_SYM=1 (experiment, off): chain A's step s+1 also waits for
+  // chain B's EVD of step s, so the EVDs strictly alternate.  Measured slower
+  // everywhere (8-GPU rank plan W=64 64.5 -> 80.0 ms per sweep, one GPU
+  // 16384^2 5.74 -> 6.02 s, profiles/r2_stagger): the one-sided stagger
+  // lets the faster chain run ahead.
+  static const bool sym = [] {
+    const char* e = getenv("SVDJ_STAGGER_SYM");
+    return e && e[0] == '1';
+  }();
+  int nr = 0;
+  hipEvent_t* evr = sym ? stagger_events(b.st, a.st, nr) : nullptr;
+  if (sym && !evr) {
+    set_error("stagger events unavailable");
+    return -100;
+  }
   const int n = a.steps > b.steps ? a.steps : b.steps;
   for (int s = 0; s < n; ++s) {
     int rc = 0;
     if (s < a.steps) {
-      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
+      if (sym && s > 0 && s - 1 < b.steps && hipStreamWaitEvent(a.st, evr[(s - 1) % nr], 0) != hipSuccess)
+        rc = -100;
+      if (!rc) rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
       if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
       if (!rc) rc = launch_apply<T, W>(a, s, mma);
     }
     if (!rc && s < b.steps) {
       if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
       if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric);
+      if (!rc && sym && s + 1 < a.steps && hipEventRecord(evr[s % nr], b.st) != hipSuccess) rc = -100;
       if (!rc) rc = launch_apply<T, W>(b, s, mma);
     }
     if (rc) {

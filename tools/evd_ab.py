@@ -22,6 +22,7 @@ p.add_argument("--m", type=int, default=None)
 p.add_argument("--block", type=int, default=32)
 p.add_argument("--dtype", default="fp32")
 p.add_argument("--sweeps", type=int, default=2)
+p.add_argument("--order", default="bipartite", choices=["cyclic", "bipartite"])
 a = p.parse_args()
 K = svdj.ops.kernels
 dt = torch.float32 if a.dtype == "fp32" else torch.float64
@@ -38,12 +39,12 @@ K.set_identity(Vt, n)
 D = K.col_norms2(At, m)
 tol = svdj.utils.metrics.default_tol(dt, m)
 metric = K.new_metric(dev)
-K.block_steps(At, Vt, D, m, pairs, W, modes, tol, 1, metric)  # warm
+K.block_steps(At, Vt, D, m, pairs, W, modes, tol, 1, metric, inner_order=a.order)  # warm
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for _ in range(a.sweeps):
-    K.block_steps(At, Vt, D, m, pairs, W, modes, tol, 1, metric)
+    K.block_steps(At, Vt, D, m, pairs, W, modes, tol, 1, metric, inner_order=a.order)
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / a.sweeps
