@@ -109,3 +109,24 @@ def test_native_plan_matches_python(P):
             else:
                 want.append([0, it.stream, *hv(it), -1, -1, -1])
         assert _native_plan(P, g) == want
+
+
+def test_native_block_rule_matches_python():
+    """bin/svdj_dist_main picks the block width with svdj_dist_choose_block,
+    the Python solvers with models.block.choose_block: same rule."""
+    import ctypes
+    import importlib
+    import torch
+    b = importlib.import_module("svd-jacobi-mpi-cuda_amd._build")
+    try:
+        b.build_dist()
+    except (FileNotFoundError, RuntimeError) as e:
+        pytest.skip(f"native distributed library not buildable here: {e}")
+    lib = ctypes.CDLL(str(b.DIST_LIB))
+    choose = svdj.models.block.choose_block
+    for dt, code in ((torch.float32, 0), (torch.float64, 1)):
+        for world in (1, 2, 4, 8):
+            for m, n in ((4096, 4096), (8192, 8192), (12288, 12288), (16384, 16384),
+                         (32768, 8192), (65536, 65536), (20000, 20000)):
+                assert lib.svdj_dist_choose_block(code, world, m, n) == choose(dt, n // world, m), \
+                    (dt, world, m, n)
