@@ -227,6 +227,9 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
 //     block steps;
 //   * the diagonal never lives in G: it travels in the rotation records (a
 //     rotation of slot a changes only d_first and d_second).
+#ifndef SVDJ_EVD_QALL
+#define SVDJ_EVD_QALL 0
+#endif
 #ifndef SVDJ_EVD_THREADS_32
 #define SVDJ_EVD_THREADS_32 1024
 #endif
@@ -594,7 +597,14 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   constexpr int R = O::R;               // steps per sweep
   constexpr int NTRI = N * (N - 1) / 2;
   constexpr int GPW = SVDJ_WAVE / W;    // Q row groups per wave
-  constexpr int NGRP = (NWAVE - 1) * GPW;  // Q row groups (waves 1..NWAVE-1)
+  // Q row groups: waves 1..NWAVE-1, or every wave (SVDJ_EVD_QALL).  Since
+  // the step loop is unrolled the solver wave is no longer the slowest
+  // (16384^2 8-GPU shape, W=64: wave 0 1357 cycles per step, a Q wave ~1440
+  // of G update + ~300 of Q), but giving it Q rows measured neutral
+  // (profiles/r2_evd_unroll): the step is bound by the G update's LDS
+  // traffic, not by the Q rows.
+  constexpr int QW0 = SVDJ_EVD_QALL ? 0 : 1;  // first Q wave
+  constexpr int NGRP = (NWAVE - QW0) * GPW;
   constexpr int RPL = (N + NGRP - 1) / NGRP;  // Q rows per lane (the last group may idle)
   constexpr int MAXOFF = EvdDeal<W, NT, ORD>::MAXOFF;
   static_assert(W >= 4 && W <= 64 && NWAVE >= 2, "EVD geometry");
@@ -757,9 +767,9 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   T pend = T(0);
 
   // ---- slot layout state of the register Q (waves 1..NWAVE-1)
-  const bool qlane = wave > 0;
+  const bool qlane = wave >= QW0;
   const int slot = lane % W;
-  const int grp = (wave - 1) * GPW + lane / W;
+  const int grp = (wave - QW0) * GPW + lane / W;
   int pf = O::first0(slot);   // first player of this slot
   int ps = O::second0(slot);  // second player
   QT qf[RPL], qs[RPL];
@@ -881,7 +891,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     constexpr int b = decltype(parity)::value, nb = b ^ 1;
     EVD_T(0);
     const bool last = st + 1 == R;  // this phase solves step 0 of the next sweep
-    if (wave == 0) {
+    if (wave == 0 && !SVDJ_EVD_QALL) {
       // solver wave: its duty blocks (lanes < W, j = 0) and nothing else of Q
       update_blocks(b, nb, true, last);
       if (last) {  // every rotation of sweep sw is decided by now
@@ -891,6 +901,29 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         racc_next = 0;
       }
       EVD_T(1);
+      EVD_T(2);
+      EVD_ACC(1, 1, 2);
+      EVD_ACC(0, 0, 1);
+    } else if (wave == 0) {
+      // solver wave with Q rows: duty blocks, then its Q share
+      const QT cq = rcq[b][slot], sq = rsq[b][slot];
+      update_blocks(b, nb, true, last);
+      if (last) {
+        const int rot = __any(racc) ? 1 : 0;
+        if (lane == 0) rot_flag[sw & 1] = rot;
+        racc = racc_next;
+        racc_next = 0;
+      }
+      EVD_T(1);
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) {
+        const QT x = qf[i], y = qs[i];
+        qf[i] = cq * x - sq * y;
+        qs[i] = sq * x + cq * y;
+      }
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
+      O::move(pf, ps, slot);
       EVD_T(2);
       EVD_ACC(1, 1, 2);
       EVD_ACC(0, 0, 1);
