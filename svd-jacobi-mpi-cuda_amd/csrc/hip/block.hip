@@ -227,6 +227,12 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
 //     block steps;
 //   * the diagonal never lives in G: it travels in the rotation records (a
 //     rotation of slot a changes only d_first and d_second).
+// Two values of one type, aligned to their combined size (one LDS access).
+template <typename T>
+struct alignas(2 * sizeof(T)) Pair2 {
+  T x, y;
+};
+
 #ifndef SVDJ_EVD_QALL
 #define SVDJ_EVD_QALL 0
 #endif
@@ -622,8 +628,11 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   // the data precision steer G, (cq, sq) in the Q precision rotate Q (fp64
   // for fp32 data: normalised once, by the solver), (dp, dq) are the slot's
   // diagonals after its rotation
-  __shared__ T rc[2][W], rs[2][W], rdp[2][W], rdq[2][W];
-  __shared__ QT rcq[2][W], rsq[2][W];
+  // records as pairs: one 8/16-byte LDS access per (c, s), (dp, dq), (cq, sq)
+  using T2 = Pair2<T>;
+  using QT2 = Pair2<QT>;
+  __shared__ T2 rcs[2][W], rdd[2][W];
+  __shared__ QT2 rq[2][W];
   __shared__ int rot_flag[2];  // any rotation in sweep (parity), written by wave 0
   __shared__ float wmax[NWAVE];
   __shared__ int wneed[NWAVE];
@@ -782,17 +791,13 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 
   // ---- prologue: step 0's rotations from the assembled G
   auto publish = [&](int b, int ns, T c, T sn, T t, T dfp, T dsp) {
-    rc[b][ns] = c;
-    rs[b][ns] = sn;
-    rdp[b][ns] = dfp;
-    rdq[b][ns] = dsp;
+    rcs[b][ns] = T2{c, sn};
+    rdd[b][ns] = T2{dfp, dsp};
     if constexpr (sizeof(QT) == sizeof(T)) {
-      rcq[b][ns] = c;
-      rsq[b][ns] = sn;
+      rq[b][ns] = QT2{c, sn};
     } else {  // fp64 (c, s) of the fp32 t, normalised in fp64
       const double td = (double)t, c64 = rsqrt64(fma(td, td, 1.0));
-      rcq[b][ns] = c64;
-      rsq[b][ns] = td * c64;
+      rq[b][ns] = QT2{c64, td * c64};
     }
   };
   // rotations seen by this solver lane in the current / next inner sweep
@@ -837,15 +842,17 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     k.g01 = gat(b, rd[j][1]);
     k.g10 = gat(b, rd[j][2]);
     k.g11 = gat(b, rd[j][3]);
-    k.ca = rc[b][ba[j]];
-    k.sa = rs[b][ba[j]];
-    k.cb = rc[b][bb[j]];
-    k.sb = rs[b][bb[j]];
+    const T2 ra = rcs[b][ba[j]], rb = rcs[b][bb[j]];
+    k.ca = ra.x;
+    k.sa = ra.y;
+    k.cb = rb.x;
+    k.sb = rb.y;
     k.dx = k.dy = T(0);
     if (duty) {
       const int e = sv >> 8;
-      k.dx = (e >> 1) ? rdq[b][ba[j]] : rdp[b][ba[j]];
-      k.dy = (e & 1) ? rdq[b][bb[j]] : rdp[b][bb[j]];
+      const T2 da = rdd[b][ba[j]], db = rdd[b][bb[j]];
+      k.dx = (e >> 1) ? da.y : da.x;
+      k.dy = (e & 1) ? db.y : db.x;
     }
   };
   auto finish_block = [&](int j, int nb, bool duty, bool last, const BlkIn& k) {
@@ -906,7 +913,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       EVD_ACC(0, 0, 1);
     } else if (wave == 0) {
       // solver wave with Q rows: duty blocks, then its Q share
-      const QT cq = rcq[b][slot], sq = rsq[b][slot];
+      const QT2 rqs = rq[b][slot];
+      const QT cq = rqs.x, sq = rqs.y;
       update_blocks(b, nb, true, last);
       if (last) {
         const int rot = __any(racc) ? 1 : 0;
@@ -929,7 +937,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       EVD_ACC(0, 0, 1);
     } else {
       // Q waves: this step's Q rotation (records read up front)
-      const QT cq = rcq[b][slot], sq = rsq[b][slot];
+      const QT2 rqs = rq[b][slot];
+      const QT cq = rqs.x, sq = rqs.y;
       update_blocks(b, nb, false, last);
       EVD_T(1);
       // Q <- Q J in registers (c = 1, s = 0 for no rotation)
@@ -986,8 +995,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       const int lb = (gs - 1) & 1;
       int p, q;
       O::players(tid, R - 1, p, q);
-      D[p < W ? bi * W + p : bj * W + (p - W)] = rdp[lb][tid];
-      D[q < W ? bi * W + q : bj * W + (q - W)] = rdq[lb][tid];
+      D[p < W ? bi * W + p : bj * W + (p - W)] = rdd[lb][tid].x;
+      D[q < W ? bi * W + q : bj * W + (q - W)] = rdd[lb][tid].y;
     }
   } else {
     for (int a = tid; a < N; a += NT) D[a < W ? bi * W + a : bj * W + (a - W)] = dg[a];
