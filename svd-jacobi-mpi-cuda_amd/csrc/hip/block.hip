@@ -1595,6 +1595,74 @@ static int check_dims(int m_pad, int lda, const void* V, int n_v, int ldv, int m
   return 0;
 }
 
+// N independent chains (disjoint blocks) on N streams, staggered in a
+// cascade: chain c's step s starts when chain c-1's EVD of step s is done.
+// With few pairs per step (many GPUs) every chain's gram -> EVD -> apply is
+// latency-bound; four half-size chains keep twice as many of those latency
+// chains in flight as two (parallel/pipeline.py sweep_plan(chains=4)).
+template <typename T, int W>
+static int block_stepsN_t(const Chain<T>* ch, int nch, double tol, int absmode, int max_inner,
+                          uint32_t* metric, int mma) {
+  // SVDJ_STAGGER_N: 0 = cascade (c waits on c-1), 1 = pairs (odd c waits on
+  // c-1: (0,1), (2,3) staggered as two block_steps2), 2 = none
+  static const int smode = [] {
+    const char* e = getenv("SVDJ_STAGGER_N");
+    return e ? atoi(e) : 1;
+  }();
+  auto waits = [&](int c) { return c > 0 && (smode == 0 || (smode == 1 && (c & 1))); };
+  hipEvent_t* ev[8] = {};
+  int ne[8] = {};
+  for (int c = 0; c + 1 < nch; ++c) {
+    ev[c] = stagger_events(ch[c].st, ch[c + 1].st, ne[c]);
+    if (!ev[c]) {
+      set_error("stagger events unavailable");
+      return -100;
+    }
+  }
+  int n = 0;
+  for (int c = 0; c < nch; ++c) n = ch[c].steps > n ? ch[c].steps : n;
+  for (int s = 0; s < n; ++s) {
+    for (int c = 0; c < nch; ++c) {
+      const Chain<T>& x = ch[c];
+      if (s >= x.steps) continue;
+      int rc = 0;
+      if (waits(c) && s < ch[c - 1].steps &&
+          hipStreamWaitEvent(x.st, ev[c - 1][s % ne[c - 1]], 0) != hipSuccess)
+        rc = -100;
+      if (!rc) rc = launch_gram_evd<T, W>(x, s, tol, absmode, max_inner, metric);
+      if (!rc && c + 1 < nch && waits(c + 1) && s < ch[c + 1].steps &&
+          hipEventRecord(ev[c][s % ne[c]], x.st) != hipSuccess)
+        rc = -100;
+      if (!rc) rc = launch_apply<T, W>(x, s, mma);
+      if (rc) {
+        if (rc == -100) set_error("stagger event record/wait failed");
+        return rc;
+      }
+    }
+  }
+  return 0;
+}
+
+template <typename T, int W>
+static int stepsN_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D, int nch,
+                           const int32_t* const* pairs, const int* P, const int* steps,
+                           const int32_t* const* modes, void* const* ws, const size_t* ws_bytes,
+                           void* const* streams, double tol, int absmode, int max_inner,
+                           uint32_t* metric, int mma) {
+  Chain<T> ch[8];
+  for (int c = 0; c < nch; ++c) {
+    for (int d = 0; d < c; ++d)
+      if (ws[d] == ws[c] || streams[d] == streams[c]) {
+        set_error("chains need distinct workspaces and streams");
+        return -2;
+      }
+    int rc = chain_init<T, W>(ch[c], m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs[c], P[c],
+                              steps[c], modes[c], ws[c], ws_bytes[c], mma, (hipStream_t)streams[c]);
+    if (rc) return rc;
+  }
+  return block_stepsN_t<T, W>(ch, nch, tol, absmode, max_inner, metric, mma);
+}
+
 template <typename T, int W>
 static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D,
                           const int32_t* pairs, int P, int steps, const int32_t* modes,
@@ -1662,6 +1730,34 @@ extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, 
   return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
                    tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2,
                    modes2, ws2, ws2_bytes, stream2);
+}
+
+extern "C" int svdj_block_stepsN(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                 int ldv, void* D, int nchains, const int32_t* const* pairs,
+                                 const int* P, const int* steps, const int32_t* const* modes,
+                                 void* const* ws, const size_t* ws_bytes, void* const* streams,
+                                 double tol, int tol_mode, int max_inner, uint32_t* metric,
+                                 int mma) {
+  int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
+  if (rc) return rc;
+  if (tol_mode != 0 && tol_mode != 1) {
+    set_error("bad tol_mode %d (0 relative, 1 absolute)", tol_mode);
+    return -2;
+  }
+  if (nchains < 1 || nchains > 8) {
+    set_error("nchains %d (1..8)", nchains);
+    return -2;
+  }
+#define SVDJ_STEPSN_ARGS                                                                      \
+  m_pad, A, lda, V, n_v, ldv, D, nchains, pairs, P, steps, modes, ws, ws_bytes, streams, tol, \
+      tol_mode, max_inner, metric, mma
+  if (dtype == 0 && W == 32) return stepsN_dispatch<float, 32>(SVDJ_STEPSN_ARGS);
+  if (dtype == 0 && W == 64) return stepsN_dispatch<float, 64>(SVDJ_STEPSN_ARGS);
+  if (dtype == 1 && W == 32) return stepsN_dispatch<double, 32>(SVDJ_STEPSN_ARGS);
+  if (dtype == 1 && W == 64) return stepsN_dispatch<double, 64>(SVDJ_STEPSN_ARGS);
+#undef SVDJ_STEPSN_ARGS
+  set_error("unsupported (dtype=%d, W=%d); supported: W in {32, 64}", dtype, W);
+  return -3;
 }
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,

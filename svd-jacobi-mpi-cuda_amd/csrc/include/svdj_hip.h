@@ -87,6 +87,16 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
                       double tol, int tol_mode, int max_inner_sweeps,
                       uint32_t* metric, int mma);
 
+// N (1..8) independent chains on N streams with their own workspaces,
+// staggered in a cascade: chain c's step s starts when chain c-1's EVD of
+// step s is done.  Arrays are indexed by chain; modes are host arrays.
+int svdj_block_stepsN(int dtype, int W, int m_pad, void* A, int lda, void* V,
+                      int n_v, int ldv, void* D, int nchains,
+                      const int32_t* const* pairs, const int* P, const int* steps,
+                      const int32_t* const* modes, void* const* workspace,
+                      const size_t* ws_bytes, void* const* streams, double tol,
+                      int tol_mode, int max_inner_sweeps, uint32_t* metric, int mma);
+
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
 // step, 1 = bipartite EVD in the cross steps (mode 2).  Returns sweeps, <0 on

@@ -115,6 +115,10 @@ def hip_lib():
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
               c_int, c_int, c_i32_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_int,
               c_i32_p, c_void_p, c_size_t, c_void_p, c_double, c_int, c_int, c_void_p, c_int])
+        _sig(lib, "svdj_block_stepsN", c_int,
+             [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
+              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
+              c_int, c_int, c_void_p, c_int])
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,

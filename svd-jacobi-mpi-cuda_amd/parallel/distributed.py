@@ -59,7 +59,10 @@ class DistributedBlockJacobi(Solver):
         W = self.config.block or choose_block(dtype, max(n // max(P, 1), 1), m)
         K.check_block(dtype, W)
         # pipelined sweeps split super-blocks in halves: k = B/W must be even
-        q = (4 if self.config.chains >= 2 else 2) * P * W
+        # pipelined sweeps split super-blocks in parts (halves / quarters):
+        # k = B/W must be a multiple of the part count
+        parts = self.config.chains if self.config.chains in (2, 4) else 1
+        q = 2 * max(parts, 1) * P * W
         ncols = round_up(max(n, q), q)
         B = ncols // (2 * P)
         return {"P": P, "W": W, "ncols": ncols, "B": B, "k": B // W, "m_pad": pad_rows(m),
@@ -229,7 +232,7 @@ class DistributedBlockJacobi(Solver):
         tour = tournament(P)
         pipelined = cfg.chains >= 2
         if pipelined:
-            splan = sweep_plan(P, k, tour.xslot[:, g])
+            splan = sweep_plan(P, k, tour.xslot[:, g], chains=cfg.chains)
         else:
             plans = distributed_sweep_plan(P, k)
             dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
@@ -277,7 +280,8 @@ class DistributedBlockJacobi(Solver):
         converged = False
         bufs = (rA, rV, rD)
         if pipelined:
-            ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing)
+            ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
+                                  parts=splan.parts)
 
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
@@ -289,13 +293,19 @@ class DistributedBlockJacobi(Solver):
                                mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                                inner_order=cfg.inner_order)
 
+            def run_multi(chains):
+                K.block_steps_multi(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, chains,
+                                    mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
+                                    inner_order=cfg.inner_order)
+
             if not cfg.stagger:
-                run_pair = None
+                run_pair = run_multi = None
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
                 if pipelined:
-                    t_comm += ex.run(splan, run_steps, phys, run_pair)
+                    t_comm += ex.run(splan, run_steps, phys, run_pair,
+                                     run_multi if splan.parts > 2 else None)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:
@@ -351,7 +361,7 @@ class DistributedBlockJacobi(Solver):
         key = str(dev)
         cache = self.__dict__.setdefault("_streams", {})
         if key not in cache:
-            cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
+            cache[key] = [torch.cuda.Stream(dev) for _ in range(max(2, self.config.chains))]
         return cache[key]
 
     # ------------------------------------------------------- data movement

@@ -45,12 +45,12 @@ class Task:
     pairs: np.ndarray        # (steps, pairs_per_step, 2)
     modes: list
     stream: int
-    halves: tuple            # ((slot, half), ...) touched
+    halves: tuple            # ((slot, part), ...) touched (parts are halves for 2 chains)
 
 
 @dataclass
 class Send:
-    """Exchange of half ``half`` of slot ``slot`` before round ``round``."""
+    """Exchange of part ``half`` of slot ``slot`` before round ``round``."""
     round: int
     slot: int
     half: int
@@ -61,10 +61,11 @@ class SweepPlan:
     P: int
     k: int
     items: list = field(default_factory=list)   # Task | Send, in issue order
+    parts: int = 2           # a super-block moves in this many parts (= chains)
 
 
-def _blocks(slot: int, half: int, k: int) -> list:
-    h = k // 2
+def _blocks(slot: int, half: int, k: int, parts: int = 2) -> list:
+    h = k // parts
     return list(range(slot * k + half * h, slot * k + (half + 1) * h))
 
 
@@ -77,9 +78,14 @@ def _bipartite(xs: list, ys: list) -> np.ndarray:
     return out
 
 
-def sweep_plan(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
+def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2) -> SweepPlan:
     """Items of one sweep.  ``xslot[r]`` is the slot replaced before round r
-    (r >= 1), as produced by schedule.tournament."""
+    (r >= 1), as produced by schedule.tournament.  ``chains=4``: quarters
+    instead of halves (sweep_plan4)."""
+    if chains == 4:
+        return sweep_plan4(P, k, xslot)
+    if chains != 2:
+        raise ValueError(f"pipelined sweep: 2 or 4 chains, got {chains}")
     if k < 2 or k % 2:
         raise ValueError(f"pipelined sweep needs an even block count per super-block, got {k}")
     plan = SweepPlan(P, k)
@@ -109,7 +115,97 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
     return plan
 
 
-def issue_groups(items: list, stagger: bool) -> list:
+def sweep_plan4(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
+    """Four chains: every super-block is four quarters q0..q3 (k/4 blocks).
+
+    Round 0, per slot s (chains 2s, 2s+1):  RR(q0 q1) || RR(q2 q3)   [first
+    step full], then q0 x q2 || q1 x q3, then q0 x q3 || q1 x q2.
+    Every round:  four phases t = 0..3 of I_c x S_(c+t)%4 on chain c (a
+    Latin square: each phase touches every quarter once).  The four quarters
+    of the next outgoing slot are sent after the last phase, each as soon as
+    its own last user is done.  Each
+    chain step holds k/4 pairs instead of k/2: with few pairs per step (many
+    GPUs) four shorter latency chains are in flight instead of two."""
+    if k < 4 or k % 4:
+        raise ValueError(f"4-chain sweep needs k % 4 == 0 blocks per super-block, got {k}")
+    plan = SweepPlan(P, k, parts=4)
+    q, h = k // 4, k // 2
+    rr = round_robin(h)
+    rr_modes = [1] + [0] * (h - 2)
+    for s in range(2):
+        for hh in range(2):
+            plan.items.append(Task(f"rr{s}{hh}", rr + s * k + hh * h, rr_modes, 2 * s + hh,
+                                   ((s, 2 * hh), (s, 2 * hh + 1))))
+    for pa, pb, pc, pd in ((0, 2, 1, 3), (0, 3, 1, 2)):
+        for s in range(2):
+            plan.items.append(Task(f"w{s}.{pa}{pb}", _bipartite(_blocks(s, pa, k, 4),
+                                                                 _blocks(s, pb, k, 4)),
+                                   [0] * q, 2 * s, ((s, pa), (s, pb))))
+            plan.items.append(Task(f"w{s}.{pc}{pd}", _bipartite(_blocks(s, pc, k, 4),
+                                                                 _blocks(s, pd, k, 4)),
+                                   [0] * q, 2 * s + 1, ((s, pc), (s, pd))))
+    R = 2 * P - 1
+    for r in range(R):
+        inc = int(xslot[r]) if r > 0 else 0
+        stay = 1 - inc
+        nxt = int(xslot[r + 1]) if r + 1 < R else None
+        for t in range(4):
+            for c in range(4):
+                p = (c + t) % 4
+                plan.items.append(Task(f"r{r}.T{c}{p}", _bipartite(_blocks(inc, c, k, 4),
+                                                                  _blocks(stay, p, k, 4)),
+                                       [0] * q, c, ((inc, c), (stay, p))))
+        if nxt is not None:
+            # after every user is issued, in the same order on every GPU (the
+            # grouped send/recv of part j must match across ranks); each send
+            # still starts as soon as ITS part's last user is done
+            plan.items.extend(Send(r + 1, nxt, part) for part in range(4))
+    return plan
+
+
+def issue_groups(items: list, stagger: bool, max_group: int = 2) -> list:
+    """The plan's items regrouped for issue: a Task, a Send, or a tuple of up
+    to ``max_group`` tasks issued jointly as staggered chains
+    (ops.kernels.block_steps2 / block_steps_multi).
+
+    Greedy: a task is grouped with the following tasks (Sends in between are
+    skipped) while each runs on a new stream, touches parts disjoint from the
+    group's, and no skipped Send concerns its parts; the skipped Sends are
+    issued after the group (they only wait on events of earlier users of
+    their part, so the delay is host-side only).  For two chains this pairs
+    rr0+rr1, T01+T10, the last round's T00+T11 / T01+T10, and T11 of a round
+    with T00 of the next across the half-1 Send."""
+    out = []
+    i, n = 0, len(items)
+    while i < n:
+        it = items[i]
+        if not (stagger and isinstance(it, Task)):
+            out.append(it)
+            i += 1
+            continue
+        group, streams, parts = [it], {it.stream}, set(it.halves)
+        skipped, last, j = [], i, i + 1
+        while j < n and len(group) < max_group:
+            x = items[j]
+            if isinstance(x, Send):
+                skipped.append((j, x))
+                j += 1
+                continue
+            if (x.stream in streams or set(x.halves) & parts
+                    or any((sd.slot, sd.half) in x.halves for _, sd in skipped)):
+                break
+            group.append(x)
+            streams.add(x.stream)
+            parts |= set(x.halves)
+            last = j
+            j += 1
+        out.append(tuple(group) if len(group) > 1 else it)
+        out.extend(sd for idx, sd in skipped if idx < last)
+        i = last + 1
+    return out
+
+
+def _issue_groups_pairs(items: list, stagger: bool) -> list:
     """The plan's items regrouped for issue: a Task, a Send, or a (Task, Task)
     pair issued jointly as two staggered chains (ops.kernels.block_steps2).
 
@@ -149,9 +245,10 @@ def check_plan_coverage(plans: list, tour) -> None:
     exactly once.  Raises AssertionError."""
     P = len(plans)
     k = plans[0].k
-    h = k // 2
-    # place[g][slot][half] = (super-block, half) currently resident
-    place = [[[(int(tour.held[0, g, s]), hh) for hh in range(2)] for s in range(2)]
+    parts = plans[0].parts
+    h = k // parts
+    # place[g][slot][part] = (super-block, part) currently resident
+    place = [[[(int(tour.held[0, g, s]), hh) for hh in range(parts)] for s in range(2)]
              for g in range(P)]
     met = {}
     n_items = len(plans[0].items)
@@ -204,18 +301,20 @@ class PipelineExecutor:
     trailed the moment the consumer stream was ready -- the part of the
     exchange not hidden under compute)."""
 
-    def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour, timing: bool = False):
+    def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour, timing: bool = False,
+                 parts: int = 2):
         self.comm, self.streams = comm, streams
         self.At, self.Vt, self.D = At, Vt, D
         self.k, self.W, self.tour = k, W, tour
-        self.hB = k // 2 * W
+        self.parts = parts
+        self.hB = k // parts * W
         dev = At.device
         self.cuda = dev.type == "cuda"
         hB = self.hB
         self.rbuf = [(torch.empty(hB, At.shape[1], dtype=At.dtype, device=dev),
                       torch.empty(hB, Vt.shape[1], dtype=Vt.dtype, device=dev) if Vt is not None
                       else None,
-                      torch.empty(hB, dtype=D.dtype, device=dev)) for _ in range(2)]
+                      torch.empty(hB, dtype=D.dtype, device=dev)) for _ in range(parts)]
         self.dev_pairs = {}  # item index -> device pairs (the plan is fixed per solve)
         self._groups = {}
         self.comm_stream = torch.cuda.Stream(dev) if self.cuda and comm.distributed else None
@@ -237,7 +336,7 @@ class PipelineExecutor:
             self.dev_pairs[i] = t
         return t
 
-    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
+    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None, run_multi=None) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
         steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
         independent chains staggered, ``a``/``b`` = (pairs, modes, slot,
@@ -262,14 +361,15 @@ class PipelineExecutor:
         index = {id(it): i for i, it in enumerate(plan.items)}
         groups = self._groups.get(id(plan))
         if groups is None:
-            groups = issue_groups(plan.items, run_pair is not None)
+            groups = issue_groups(plan.items, run_pair is not None,
+                                  max_group=plan.parts if run_multi is not None else 2)
             self._groups[id(plan)] = groups
         for it in groups:
             if isinstance(it, Send):
                 tc = time.perf_counter()
                 self._send(it, last, pending)
                 halves_done[it.round] = halves_done.get(it.round, 0) + 1
-                if halves_done[it.round] == 2:
+                if halves_done[it.round] == self.parts:
                     self._update_phys(it.round, phys)
                 t_comm += time.perf_counter() - tc
                 continue
@@ -292,6 +392,9 @@ class PipelineExecutor:
                 a, b = tasks
                 run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
                          (pairs[1], b.modes, b.stream, self.streams[b.stream]))
+            elif len(tasks) > 2:
+                run_multi([(pr, t.modes, t.stream, self.streams[t.stream])
+                           for pr, t in zip(pairs, tasks)])
             else:
                 with torch.cuda.stream(self.streams[tasks[0].stream]):
                     run_steps(pairs[0], tasks[0].modes, tasks[0].stream)

@@ -320,3 +320,41 @@ def test_svd_end_to_end_bipartite(svdj, cuda, dtype):
     r, sg, ou, ov = _E2E_BOUNDS[("block", dtype, "native")]
     assert rep["residual_rel"] < r and rep["sigma_max_abs_err_over_smax"] < sg, rep
     assert rep["orth_u_fro"] < ou and rep["orth_v_fro"] < ov, rep
+
+
+def test_block_steps_multi_chain_matches_sequential(svdj, cuda):
+    """svdj_block_stepsN: four chains on four streams, staggered in a cascade,
+    on disjoint blocks give bitwise the result of running the chains one
+    after the other on one stream."""
+    K = svdj.ops.kernels
+    W, nb, m, m_pad = 32, 16, 700, 768
+    n = nb * W
+    A0 = _rand_At(n, m_pad, m, torch.float32, cuda, seed=11)
+    rr = svdj.parallel.schedule.round_robin(4)  # 3 steps x 2 pairs on 4 blocks
+    chains = []
+    streams = [torch.cuda.Stream(cuda) for _ in range(4)]
+    for c in range(4):
+        pairs = torch.from_numpy(rr + 4 * c).to(cuda)
+        chains.append((pairs, [1, 0, 0], c, streams[c]))
+
+    def run(multi):
+        At = A0.clone()
+        Vt = torch.zeros(n, n, dtype=torch.float32, device=cuda)
+        K.set_identity(Vt, n)
+        D = K.col_norms2(At, m_pad)
+        metric = K.new_metric(cuda)
+        torch.cuda.synchronize()
+        if multi:
+            K.block_steps_multi(At, Vt, D, m_pad, W, 1e-6, 1, metric, chains, pool={},
+                                inner_order="bipartite")
+        else:
+            for pairs, modes, slot, _ in chains:
+                K.block_steps(At, Vt, D, m_pad, pairs, W, modes, 1e-6, 1, metric, slot, pool={},
+                              inner_order="bipartite")
+        torch.cuda.synchronize()
+        return At, Vt, D, K.read_metric(metric)
+
+    a1, v1, d1, m1 = run(True)
+    a0, v0, d0, m0 = run(False)
+    assert m1[1] == m0[1] > 0
+    assert torch.equal(a1, a0) and torch.equal(v1, v0) and torch.equal(d1, d0)

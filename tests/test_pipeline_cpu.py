@@ -130,3 +130,32 @@ def test_native_block_rule_matches_python():
                          (32768, 8192), (65536, 65536), (20000, 20000)):
                 assert lib.svdj_dist_choose_block(code, world, m, n) == choose(dt, n // world, m), \
                     (dt, world, m, n)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
+def test_four_chain_plan_covers_and_groups(P, k):
+    """sweep_plan4: every block pair meets once per sweep; every round's
+    tasks issue as groups of four disjoint chains; the four quarter sends of
+    a round come in the same order on every GPU."""
+    tour = schedule.tournament(P)
+    plans = [pipeline.sweep_plan(P, k, tour.xslot[:, g], chains=4) for g in range(P)]
+    pipeline.check_plan_coverage(plans, tour)
+    for pl in plans:
+        groups = pipeline.issue_groups(pl.items, True, max_group=4)
+        tasks = [g for g in groups if not isinstance(g, pipeline.Send)]
+        assert all(isinstance(g, tuple) and len(g) == 4 for g in tasks)
+        sends = [g for g in groups if isinstance(g, pipeline.Send)]
+        assert [s.half for s in sends] == [0, 1, 2, 3] * (2 * P - 2)
+
+
+def test_generalised_grouping_keeps_pairs():
+    """issue_groups with two chains groups exactly as the original pair rule."""
+    for P in (1, 2, 3, 4, 8):
+        tour = schedule.tournament(P)
+        for k in (2, 4, 6):
+            for g in range(P):
+                items = pipeline.sweep_plan(P, k, tour.xslot[:, g]).items
+                key = lambda x: tuple(map(id, x)) if isinstance(x, tuple) else id(x)  # noqa: E731
+                assert [key(x) for x in pipeline.issue_groups(items, True)] == \
+                    [key(x) for x in pipeline._issue_groups_pairs(items, True)]
