@@ -1016,8 +1016,10 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 #ifndef SVDJ_APPLY_EARLY
 #define SVDJ_APPLY_EARLY 0
 #endif
+// Q in A-operand fragment order: 0 never, 1 always, 2 for fp64 only (default:
+// fp64 W=64 apply 912 -> 845 us, fp32 W=64 319 -> 338 us, tools/gpu_r2_qfrag.sh)
 #ifndef SVDJ_APPLY_QFRAG
-#define SVDJ_APPLY_QFRAG 0
+#define SVDJ_APPLY_QFRAG 2
 #endif
 template <typename T, int W>
 __host__ __device__ constexpr int apply_threads() {
@@ -1087,18 +1089,20 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   if (r0 < r_end) load_tile(xv, r0);
 #endif
   const T* Qg = Qall + (size_t)pair * N * N;
-#if SVDJ_APPLY_QFRAG
-  // Q in A-operand fragment order: for (column tile, group of VEC k-steps,
-  // lane) the VEC operands are contiguous, one 16-byte LDS read per VEC MFMAs
+  // Q in A-operand fragment order (kQFrag): for (column tile, group of VEC
+  // k-steps, lane) the VEC operands are contiguous, one 16-byte LDS read per
+  // VEC MFMAs
+  constexpr bool kQFrag = SVDJ_APPLY_QFRAG == 1 || (SVDJ_APPLY_QFRAG == 2 && sizeof(T) == 8);
   constexpr int VEC = 16 / (int)sizeof(T);
-  for (int i = threadIdx.x; i < N * N; i += NTH) {
-    const int k = i / N, c = i % N;
-    const int kk = k / KG, kgi = k % KG, ct = c / TL, lci = c % TL;
-    Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = Qg[i];
+  if constexpr (kQFrag) {
+    for (int i = threadIdx.x; i < N * N; i += NTH) {
+      const int k = i / N, c = i % N;
+      const int kk = k / KG, kgi = k % KG, ct = c / TL, lci = c % TL;
+      Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = Qg[i];
+    }
+  } else {
+    for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
   }
-#else
-  for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
-#endif
   __syncthreads();
   if (r0 >= r_end) return;
 #if !SVDJ_APPLY_EARLY
@@ -1114,8 +1118,7 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
 #pragma unroll kCtUnroll
     for (int ct = 0; ct < NCT; ++ct) {
       typename M::acc_t acc = M::zero();
-#if SVDJ_APPLY_QFRAG
-      {
+      if constexpr (kQFrag) {
         using V4 = __attribute__((ext_vector_type(VEC))) T;
         const V4* qv = reinterpret_cast<const V4*>(Qs) + (size_t)ct * (NK / VEC) * 64 + lane;
         V4 cur = qv[0];
@@ -1127,8 +1130,7 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
           for (int e = 0; e < VEC; ++e) acc = M::mfma(cur[e], xv[g * VEC + e], acc);
           cur = nxt;
         }
-      }
-#else
+      } else {
       // Q fragments are read SVDJ_APPLY_QPD k-steps ahead of their MFMA
       // (sched_barrier keeps the order; just in time, each ds_read's latency
       // sat between two dependent MFMAs).  Two interleaved accumulation
@@ -1144,7 +1146,7 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
         acc = M::mfma(a, xv[kk], acc);
         __builtin_amdgcn_sched_barrier(0);
       }
-#endif
+      }
       const int c0 = ct * TL;
       T* dst = (c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld);
 #pragma unroll
