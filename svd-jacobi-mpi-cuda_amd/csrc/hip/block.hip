@@ -51,6 +51,27 @@ enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2 };
 template <typename T, int W>
 __host__ __device__ constexpr int gram_xsplit() { return (sizeof(T) == 8 && W == 64) ? 2 : 1; }
 
+// Rows per lane per slab of the fp32 W=64 cross Gram (16 = 64 bytes, the
+// default).  8 or 4 cut registers (208 -> 172) but measured slower end to end
+// (16384^2 1 GPU 5.76 -> 6.08 s, 8-GPU rank plan 63.8 -> 73 ms, gpu_r2_lpl.sh).
+#ifndef SVDJ_GRAM_LPL64
+#define SVDJ_GRAM_LPL64 16
+#endif
+// NV consecutive elements of one column with 16-byte vector loads.
+template <typename T, int NV>
+__device__ __forceinline__ void load_col16B(const T* __restrict__ p, T (&v)[NV]) {
+  constexpr int PER = 16 / (int)sizeof(T);
+  static_assert(NV % PER == 0, "whole 16-byte vectors");
+  const f32x4* q = reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < NV / PER; ++i) {
+    f32x4 x = q[i];
+    const T* xs = reinterpret_cast<const T*>(&x);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[i * PER + j] = xs[j];
+  }
+}
+
 template <typename T, int W, int MODE>
 __global__ __launch_bounds__(kGramThreads) void gram_kernel(
     const T* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
@@ -63,7 +84,10 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   constexpr int HTX = HT / XS;                           // x tiles of this workgroup
   constexpr int NCT = FULL ? 2 * HT : HTX + HT;          // column tiles loaded
   constexpr int NTP = FULL ? NCT * (NCT + 1) / 2 : HTX * HT;
-  constexpr int LPL = M::LPL;
+  // rows per lane per slab: 64 bytes (SVDJ_GRAM_LPL64 for the fp32 W=64
+  // cross Gram)
+  constexpr int LPL = (sizeof(T) == 4 && W == 64 && !FULL) ? SVDJ_GRAM_LPL64 : M::LPL;
+  constexpr int SR = M::KG * LPL;  // rows per wave per slab
   constexpr int SLAB = FULL ? 4 * W * W : HTX * TL * W;  // this workgroup's reduction
   constexpr int WAVES = kGramThreads / SVDJ_WAVE;
   static_assert(HT % XS == 0, "x tiles split evenly");
@@ -100,18 +124,18 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   // Software pipeline: the next 32-row slab's loads are issued before this
   // slab's MFMAs, so HBM latency overlaps matrix-core work (without it the
   // kernel ran at ~2 TB/s, latency-bound, measured on MI355X at n=16384).
-  int r0 = r_begin + wave * 32;
+  int r0 = r_begin + wave * SR;
   T v[NCT][LPL];
   if (r0 < r_end) {
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) load_col64B<T>(colp[ct] + r0, v[ct]);
+    for (int ct = 0; ct < NCT; ++ct) load_col16B<T, LPL>(colp[ct] + r0, v[ct]);
   }
-  for (; r0 < r_end; r0 += WAVES * 32) {
-    const int rn = r0 + WAVES * 32;
+  for (; r0 < r_end; r0 += WAVES * SR) {
+    const int rn = r0 + WAVES * SR;
     T vn[NCT][LPL];
     if (rn < r_end) {
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) load_col64B<T>(colp[ct] + rn, vn[ct]);
+      for (int ct = 0; ct < NCT; ++ct) load_col16B<T, LPL>(colp[ct] + rn, vn[ct]);
     }
 #pragma unroll
     for (int t = 0; t < LPL; ++t) {
