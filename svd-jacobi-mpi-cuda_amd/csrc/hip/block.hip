@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   constexpr int LDQ = N + (sizeof(T) == 8 ? 16 : 0);
   constexpr int NTH = apply_threads<T, W>();
   constexpr int WAVES = NTH / SVDJ_WAVE;
-  __shared__ T Qs[N * LDQ];
+  __shared__ alignas(16) T Qs[N * LDQ];
 
   const int pair = blockIdx.x;
   if (skip[pair]) return;
@@ -1118,14 +1118,25 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   // VEC MFMAs
   constexpr bool kQFrag = SVDJ_APPLY_QFRAG == 1 || (SVDJ_APPLY_QFRAG == 2 && sizeof(T) == 8);
   constexpr int VEC = 16 / (int)sizeof(T);
+  // 16-byte loads (Q is 16-byte aligned: N*N elements per pair)
+  using QV = __attribute__((ext_vector_type(VEC))) T;
+  const QV* Qgv = reinterpret_cast<const QV*>(Qg);
   if constexpr (kQFrag) {
-    for (int i = threadIdx.x; i < N * N; i += NTH) {
-      const int k = i / N, c = i % N;
-      const int kk = k / KG, kgi = k % KG, ct = c / TL, lci = c % TL;
-      Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = Qg[i];
+    for (int iv = threadIdx.x; iv < N * N / VEC; iv += NTH) {
+      const QV q = Qgv[iv];
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        const int i = iv * VEC + u;
+        const int k = i / N, c = i % N;
+        const int kk = k / KG, kgi = k % KG, ct = c / TL, lci = c % TL;
+        Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = q[u];
+      }
     }
   } else {
-    for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
+    for (int iv = threadIdx.x; iv < N * N / VEC; iv += NTH) {
+      const int i = iv * VEC;  // VEC consecutive columns of one row (N % VEC == 0)
+      *reinterpret_cast<QV*>(&Qs[(i / N) * LDQ + (i % N)]) = Qgv[iv];
+    }
   }
   __syncthreads();
   if (r0 >= r_end) return;
