@@ -1488,29 +1488,46 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
   return 0;
 }
 
+// part: 0 = A and V rows in one launch, 1 = A rows only, 2 = V rows only
+// (on stream st; the V rows are then addressed as the kernel's "A" region)
 template <typename T, int W>
-static int launch_apply(const Chain<T>& c, int s, int mma) {
+static int launch_apply(const Chain<T>& c, int s, int mma, int part = 0,
+                        hipStream_t st = nullptr) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
-  const dim3 grid(c.P, c.g.a_chunks + c.g.v_chunks);
-  const int nv = c.V ? c.n_v : 0;
+  if (!st) st = c.st;
+  T* X = c.A;
+  int ldx = c.lda, xch = c.g.a_chunks, xrows = c.g.rows_a, xpad = c.m_pad;
+  T* Y = c.V;
+  int nv = c.V ? c.n_v : 0, ych = c.g.v_chunks;
+  if (part == 1) {
+    Y = nullptr;
+    nv = ych = 0;
+  } else if (part == 2) {
+    if (!c.V) return 0;
+    X = c.V;
+    ldx = c.ldv;
+    xch = c.g.v_chunks;
+    xrows = c.g.rows_v;
+    xpad = c.n_v;
+    Y = nullptr;
+    nv = ych = 0;
+  }
+  const dim3 grid(c.P, xch + ych);
   if constexpr (sizeof(T) == 4) {
     if (mma == 1 || mma == 2) {
       if (mma == 1)
-        hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, c.st, c.A,
-                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
-                           pr, c.Qb[b], c.skipb[b]);
+        hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, st, X, ldx,
+                           xch, xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
       else
-        hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, c.st, c.A,
-                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
-                           pr, c.Qb[b], c.skipb[b]);
+        hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, st, X, ldx,
+                           xch, xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
       SVDJ_LAUNCH_CHECK();
       return 0;
     }
   }
-  hipLaunchKernelGGL((apply_kernel<T, W>), grid, dim3(apply_threads<T, W>()), 0, c.st, c.A, c.lda,
-                     c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv, pr, c.Qb[b],
-                     c.skipb[b]);
+  hipLaunchKernelGGL((apply_kernel<T, W>), grid, dim3(apply_threads<T, W>()), 0, st, X, ldx, xch,
+                     xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
   SVDJ_LAUNCH_CHECK();
   return 0;
 }
@@ -1572,6 +1589,73 @@ static hipEvent_t* stagger_events(hipStream_t rec, hipStream_t wait, int& n) {
   return r->ev;
 }
 
+// ---- deferred V rotation (SVDJ_VSTREAM=1).  The next step's Gram reads A
+// only, so a chain can run apply(V rows, s) on a side stream while its
+// gram / EVD of step s+1 proceed: the side stream waits for EVD(s) (Q ready),
+// EVD(s+2) waits for apply(V, s) (it rewrites the same Q / skip buffer), and
+// the chain stream joins the side stream at the end of the call.
+static hipStream_t side_stream(hipStream_t st) {
+  static std::mutex mu;
+  static std::vector<std::pair<hipStream_t, hipStream_t>> m;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& x : m)
+    if (x.first == st) return x.second;
+  int sdev = 0, cur = 0;
+  if (hipStreamGetDevice(st, &sdev) != hipSuccess || hipGetDevice(&cur) != hipSuccess) return nullptr;
+  if (sdev != cur && hipSetDevice(sdev) != hipSuccess) return nullptr;
+  hipStream_t v = nullptr;
+  const bool ok = hipStreamCreateWithFlags(&v, hipStreamNonBlocking) == hipSuccess;
+  if (sdev != cur) (void)hipSetDevice(cur);
+  if (!ok) return nullptr;
+  m.push_back({st, v});
+  return v;
+}
+static bool vstream_on() {
+  static const bool on = [] {
+    const char* e = getenv("SVDJ_VSTREAM");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+template <typename T>
+struct VSide {
+  hipStream_t vst = nullptr;
+  hipEvent_t *qready = nullptr, *vdone = nullptr;
+  int nq = 0, nv = 0;
+  bool init(const Chain<T>& c) {
+    if (!c.V || !vstream_on()) return true;
+    vst = side_stream(c.st);
+    if (!vst) return false;
+    qready = stagger_events(c.st, vst, nq);
+    vdone = stagger_events(vst, c.st, nv);
+    return qready && vdone;
+  }
+};
+// gram + EVD of step s, then the apply (A rows on the chain stream, V rows
+// on the side stream when it is enabled)
+template <typename T, int W>
+static int step_deferred(const Chain<T>& c, VSide<T>& v, int s, double tol, int absmode,
+                         int max_inner, uint32_t* metric, int mma, hipEvent_t after_evd) {
+  if (v.vst && s >= 2 && hipStreamWaitEvent(c.st, v.vdone[(s - 2) % v.nv], 0) != hipSuccess)
+    return -100;
+  int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric);
+  if (rc) return rc;
+  if (after_evd && hipEventRecord(after_evd, c.st) != hipSuccess) return -100;
+  if (!v.vst) return launch_apply<T, W>(c, s, mma);
+  if (hipEventRecord(v.qready[s % v.nq], c.st) != hipSuccess) return -100;
+  rc = launch_apply<T, W>(c, s, mma, 1);
+  if (rc) return rc;
+  if (hipStreamWaitEvent(v.vst, v.qready[s % v.nq], 0) != hipSuccess) return -100;
+  rc = launch_apply<T, W>(c, s, mma, 2, v.vst);
+  if (rc) return rc;
+  return hipEventRecord(v.vdone[s % v.nv], v.vst) == hipSuccess ? 0 : -100;
+}
+template <typename T>
+static int join_side(const Chain<T>& c, const VSide<T>& v) {
+  if (!v.vst || c.steps <= 0) return 0;
+  return hipStreamWaitEvent(c.st, v.vdone[(c.steps - 1) % v.nv], 0) == hipSuccess ? 0 : -100;
+}
+
 // Two independent chains on two streams, staggered: chain B's step s starts
 // when chain A's EVD of step s has finished.  Issued separately the chains
 // run in lockstep (identical steps): both EVDs -- one workgroup per pair,
@@ -1603,26 +1687,35 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
     set_error("stagger events unavailable");
     return -100;
   }
+  VSide<T> va, vb;
+  if (!va.init(a) || !vb.init(b)) {
+    set_error("side stream / events unavailable");
+    return -100;
+  }
   const int n = a.steps > b.steps ? a.steps : b.steps;
   for (int s = 0; s < n; ++s) {
     int rc = 0;
     if (s < a.steps) {
       if (sym && s > 0 && s - 1 < b.steps && hipStreamWaitEvent(a.st, evr[(s - 1) % nr], 0) != hipSuccess)
         rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
-      if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_apply<T, W>(a, s, mma);
+      if (!rc)
+        rc = step_deferred<T, W>(a, va, s, tol, absmode, max_inner, metric, mma,
+                                 s < b.steps ? ev[s % ne] : nullptr);
     }
     if (!rc && s < b.steps) {
       if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric);
-      if (!rc && sym && s + 1 < a.steps && hipEventRecord(evr[s % nr], b.st) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_apply<T, W>(b, s, mma);
+      if (!rc)
+        rc = step_deferred<T, W>(b, vb, s, tol, absmode, max_inner, metric, mma,
+                                 sym && s + 1 < a.steps ? evr[s % nr] : nullptr);
     }
     if (rc) {
       if (rc == -100) set_error("stagger event record/wait failed");
       return rc;
     }
+  }
+  if (join_side(a, va) || join_side(b, vb)) {
+    set_error("side stream join failed");
+    return -100;
   }
   return 0;
 }
