@@ -1195,6 +1195,128 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   }
 }
 
+// ------------------------------------------- apply with X staged in LDS (fp32)
+// Alternative fp32 apply, same math as apply_kernel (Out^T = Q^T X^T, lane =
+// row), with the roles of LDS and registers swapped.  Wave w owns output column
+// tile w: its Q slice (N/2 A-operand values per lane) is loaded once into
+// registers.  The 32-row X tile, which every wave multiplies, is read once
+// per workgroup with 16-byte loads into double-buffered LDS, with one barrier
+// per tile.  The next tile's loads are in flight during this tile's MFMAs.  No
+// per-wave X tile and no prefetch copy in VGPRs, so more waves fit per SIMD
+// than in apply_kernel (selected with SVDJ_APPLY_LDSX=1).
+#ifndef SVDJ_APPLY_XPD
+#define SVDJ_APPLY_XPD 8
+#endif
+#ifndef SVDJ_APPLY_LDSX_WAVES
+#define SVDJ_APPLY_LDSX_WAVES 4
+#endif
+template <int W>
+__global__ __launch_bounds__(4 * W) __attribute__((amdgpu_waves_per_eu(SVDJ_APPLY_LDSX_WAVES)))
+void apply_ldsx_kernel(
+    float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
+    int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
+    const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
+  using M = Mfma<float>;
+  constexpr int N = 2 * W;        // columns of X = [A_bi A_bj]
+  constexpr int NK = N / 2;       // k values per lane (KG = 2)
+  constexpr int NTH = 4 * W;      // N / 32 waves, one per output column tile
+  constexpr int TILE_F = N * 32;  // floats per 32-row X tile, stored [k][row]
+  constexpr int LPT = TILE_F / 4 / NTH;  // 16-byte loads per thread per tile
+  static_assert(LPT == 4 && NTH % 8 == 0, "loader mapping");
+  __shared__ alignas(16) float Xs[2][TILE_F];
+
+  const int pair = blockIdx.x;
+  if (skip[pair]) return;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  int chunk = blockIdx.y;
+  float* base;
+  int ld, r_begin, r_end;
+  if (chunk < a_chunks) {
+    base = A;
+    ld = lda;
+    r_begin = chunk * rows_a;
+    r_end = min(m_pad, r_begin + rows_a);
+  } else {
+    chunk -= a_chunks;
+    base = V;
+    ld = ldv;
+    r_begin = chunk * rows_v;
+    r_end = min(n_v, r_begin + rows_v);
+  }
+  if (r_begin >= r_end) return;
+  const int t = threadIdx.x, lane = t & 63, ct = t >> 6;
+  const int lc = M::lane_col(lane), kg = M::lane_kg(lane);
+  float* const xi = base + (size_t)bi * W * ld;
+  float* const xj = base + (size_t)bj * W * ld;
+
+  // loader: 16-byte chunk i*NTH + t of the tile is column k_i = i*NTH/8 + t/8,
+  // rows 4*(t%8) .. +3; k_i < W exactly for i < 2 (t/8 < W/2)
+  const int lrow = 4 * (t & 7);
+  uint32_t goff[LPT];
+  int soff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int k = i * (NTH / 8) + (t >> 3);
+    goff[i] = (uint32_t)((k < W ? k : k - W) * ld + lrow);
+    soff[i] = k * 32 + lrow;
+  }
+  float4 lr[LPT];
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i)
+      lr[i] = *reinterpret_cast<const float4*>((i < 2 ? xi : xj) + goff[i] + (uint32_t)r0);
+  };
+  auto lstore = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) *reinterpret_cast<float4*>(&Xs[b][soff[i]]) = lr[i];
+  };
+  gload(r_begin);
+
+  // Q slice of column tile ct: q[kk] = Q[2kk + kg][32 ct + lc]
+  const float* Qg = Qall + (size_t)pair * N * N + kg * N + ct * 32 + lc;
+  float q[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) q[kk] = Qg[(size_t)kk * 2 * N];
+
+  const int c0 = ct * 32;
+  float* const dst = c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld;
+  const uint32_t st_off = (uint32_t)(M::acc_row_lane(lane) * ld + lc);
+  lstore(0);
+  __syncthreads();
+  constexpr int PD = SVDJ_APPLY_XPD < NK ? SVDJ_APPLY_XPD : NK;
+  for (int it = 0, r0 = r_begin;; ++it, r0 += 32) {
+    const bool more = r0 + 32 < r_end;  // uniform over the workgroup
+    if (more) gload(r0 + 32);
+    // B operand of lane (kg, lc) at step kk: X[row lc][k = 2kk + kg]
+    const float* xs = &Xs[it & 1][kg * 32 + lc];
+    float xa[PD];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) xa[i] = xs[i * 64];
+    typename M::acc_t acc = M::zero();
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const float b = xa[kk % PD];
+      if (kk + PD < NK) xa[kk % PD] = xs[(kk + PD) * 64];
+      acc = M::mfma(q[kk], b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int e = 0; e < M::NACC; ++e)
+      dst[(size_t)M::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = acc[e];
+    if (!more) break;
+    lstore((it + 1) & 1);  // that buffer's last readers passed the previous barrier
+    __syncthreads();
+  }
+}
+
+static bool apply_ldsx_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SVDJ_APPLY_LDSX");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 // -------------------------------------------------- apply on bf16 matrix cores
 // fp32 data, bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate):
 // every operand is split into NP round-to-nearest bf16 parts,
@@ -1522,6 +1644,14 @@ static int launch_apply(const Chain<T>& c, int s, int mma, int part = 0,
       else
         hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, st, X, ldx,
                            xch, xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
+      SVDJ_LAUNCH_CHECK();
+      return 0;
+    }
+    // 16-byte X loads: leading dimensions and base pointers 16-byte aligned
+    if (apply_ldsx_enabled() && ldx % 4 == 0 && (nv == 0 || c.ldv % 4 == 0) &&
+        ((uintptr_t)X | (uintptr_t)Y) % 16 == 0) {
+      hipLaunchKernelGGL((apply_ldsx_kernel<W>), grid, dim3(4 * W), 0, st, X, ldx, xch, xrows,
+                         xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
       SVDJ_LAUNCH_CHECK();
       return 0;
     }
@@ -2107,7 +2237,15 @@ extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld
   else if (dtype == 0 && mma == 2 && W == 32)
     hipLaunchKernelGGL((apply_split_kernel<32, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
-  else if (dtype == 0 && mma == 0 && W == 64)
+  else if (dtype == 0 && mma == 0 && apply_ldsx_enabled() && (W == 32 || W == 64) &&
+           ld % 4 == 0 && (uintptr_t)X % 16 == 0) {
+    if (W == 64)
+      hipLaunchKernelGGL((apply_ldsx_kernel<64>), grid, dim3(256), 0, st, (float*)X, ld, chunks,
+                         rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+    else
+      hipLaunchKernelGGL((apply_ldsx_kernel<32>), grid, dim3(128), 0, st, (float*)X, ld, chunks,
+                         rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+  } else if (dtype == 0 && mma == 0 && W == 64)
     hipLaunchKernelGGL((apply_kernel<float, 64>), grid, dim3(apply_threads<float, 64>()), 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
   else if (dtype == 0 && mma == 0 && W == 32)
