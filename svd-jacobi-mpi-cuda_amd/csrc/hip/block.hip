@@ -228,6 +228,124 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   }
 }
 
+// ------------------------------------------------- gram, LDS-staged (fp32)
+// Cross Gram C = A_bi^T A_bj for fp32 W = 64 with the rows streamed through
+// LDS by LDS-DMA (global_load_lds_dwordx4), the form the CDNA4 playbook gives
+// for an MFMA operand that is read once: the register-fragment loads of
+// gram_kernel touch 32 columns x 16 bytes per instruction (32 partial cache
+// lines) and keep one 16 KB slab per wave in flight; they reached ~2.4-2.9
+// TB/s (profiles/r1_s4_pmc).  Here every wave instruction fetches 8 whole
+// 128-byte column segments, a 4-deep ring keeps 3 stages (48 KB) per
+// workgroup in flight without spending VGPRs, and each wave owns one 32 x 32
+// output tile, written straight to its slab (no cross-wave reduction).
+//
+// Stage = 32 rows x 128 columns (block bi's 64, then bj's 64) = 16 KB, one
+// 128-byte line per column.  Chunk q (rows 4q..4q+3) of column c sits at
+// 16-byte slot q ^ ((c >> 1) & 7) of the column's line: the fragment reads
+// (ds_read_b128, lanes = 16 columns per LDS cycle group) are then
+// conflict-free, and the DMA keeps its lane-linear LDS destination because
+// the swizzle is applied to the per-lane GLOBAL address.  MFMA u = 4v + e of
+// a stage takes row 8v + e (k = 0 lanes) and 8v + 4 + e (k = 1): each lane
+// reads chunk 2v + k of its column once per 4 MFMAs.
+//
+// Ordering (one barrier per stage): wait for this wave's DMAs of stage it
+// (counted vmcnt: the 2 later stages stay in flight) -> s_barrier (every
+// wave's stage-it DMAs retired; every wave's reads of stage it-1 retired by
+// its lgkmcnt(0)) -> DMA stage it+3 into stage it-1's buffer -> read + MFMA.
+// Raw s_barrier, not __syncthreads(): the latter's fence would drain the
+// in-flight DMAs (vmcnt(0)).  All LDS of the kernel is this one array.
+constexpr int kGramLdsKT = 32;  // rows per stage
+
+__device__ __forceinline__ void gram_lds_wait(int ahead) {
+  // this wave issued 4 DMAs per stage; `ahead` later stages may stay in flight
+  if (ahead >= 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (ahead == 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NS>  // ring depth: NS - 1 stages in flight (2..4)
+__global__ __launch_bounds__(kGramThreads) void gram_lds_kernel(
+    const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
+    int rows_per_chunk, float* __restrict__ slabs) {
+  static_assert(NS >= 2 && NS <= 4, "gram ring depth");
+  constexpr int W = 64, KT = kGramLdsKT;
+  constexpr int STAGE = 2 * W * KT;  // floats per stage
+  __shared__ __attribute__((aligned(16))) float lds[NS * STAGE];
+
+  const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(m_pad, r_begin + rows_per_chunk);
+  const int nst = (r_end - r_begin) / KT;
+
+  // DMA source of this lane: instruction d (0..3) of this wave covers stage
+  // columns 32 * wave + 8 d .. +7; lane -> column + 8 * (lane >> 3), slot lane & 7
+  const float* src[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int c = 32 * wave + 8 * d + (lane >> 3);
+    const int q = (lane & 7) ^ ((c >> 1) & 7);
+    const int col = (c < W ? bi : bj) * W + (c & (W - 1));
+    src[d] = A + (size_t)col * lda + r_begin + 4 * q;
+  }
+  auto issue = [&](int s) {  // stage s -> buffer s % NS
+    float* dst = lds + (s % NS) * STAGE + (32 * wave) * KT;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      __builtin_amdgcn_global_load_lds(src[d] + (size_t)s * KT, dst + 8 * d * KT, 16, 0, 0);
+  };
+
+  // this wave's output tile: X columns 32 a.., Y columns 32 b..
+  const int a = wave >> 1, b = wave & 1;
+  const int i = lane & 31, k = lane >> 5;
+  const int cx = 32 * a + i, cy = W + 32 * b + i;
+  int offx[4], offy[4];  // float offsets of chunk 2v + k inside a stage
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int q = 2 * v + k;
+    offx[v] = cx * KT + 4 * (q ^ ((cx >> 1) & 7));
+    offy[v] = cy * KT + 4 * (q ^ ((cy >> 1) & 7));
+  }
+
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+
+  for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
+  for (int it = 0; it < nst; ++it) {
+    const int ahead = min(nst - 1 - it, NS - 2);
+    gram_lds_wait(ahead);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + NS - 1 < nst) issue(it + NS - 1);
+    const float* st = lds + (it % NS) * STAGE;
+    f32x4 xv[4], yv[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      xv[v] = *reinterpret_cast<const f32x4*>(st + offx[v]);
+      yv[v] = *reinterpret_cast<const f32x4*>(st + offy[v]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[v][e], yv[v][e], acc, 0, 0, 0);
+    // this wave's reads of the stage are retired before the next barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  float* out = slabs + ((size_t)pair * nchunk + chunk) * (W * W);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * k;
+    out[r * W + 32 * b + i] = acc[e];
+  }
+}
+
 // -------------------------------------------------------------------- evd
 // The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair, as a
 // cyclic parallel Jacobi (circle-method round robin: W disjoint rotations per
@@ -1576,6 +1694,40 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   return 0;
 }
 
+// The LDS-staged cross Gram (fp32 W = 64), opt-in: SVDJ_GRAM_LDS=<ring depth
+// 2..4>.  Needs 16-byte aligned column starts and chunk rows a multiple of the
+// stage height.
+static int gram_lds_stages() {
+  static const int ns = [] {
+    const char* e = getenv("SVDJ_GRAM_LDS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 2 && v <= 4 ? v : 0;
+  }();
+  return ns;
+}
+static void launch_gram_lds(int ns, dim3 grid, hipStream_t st, const float* A, int lda, int m_pad,
+                            const int32_t* pairs, int rows, float* slabs) {
+  if (ns == 2)
+    hipLaunchKernelGGL(gram_lds_kernel<2>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
+                       rows, slabs);
+  else if (ns == 3)
+    hipLaunchKernelGGL(gram_lds_kernel<3>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
+                       rows, slabs);
+  else
+    hipLaunchKernelGGL(gram_lds_kernel<4>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
+                       rows, slabs);
+}
+template <typename T, int W>
+static bool gram_lds_ok(const Chain<T>& c) {
+  if constexpr (!(std::is_same<T, float>::value && W == 64)) {
+    (void)c;
+    return false;
+  } else {
+    return gram_lds_stages() && c.lda % 4 == 0 && (uintptr_t)c.A % 16 == 0 &&
+           c.g.grows % kGramLdsKT == 0 && c.m_pad % kGramLdsKT == 0;
+  }
+}
+
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
 template <typename T, int W>
@@ -1593,6 +1745,9 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
     else
       hipLaunchKernelGGL((gram_kernel<T, W, GRAM_FULL>), dim3(c.P, c.g.gchunks),
                          dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  } else if (gram_lds_ok<T, W>(c)) {
+    launch_gram_lds(gram_lds_stages(), dim3(c.P, c.g.gchunks), c.st, (const float*)c.A, c.lda,
+                    c.m_pad, pr, c.g.grows, (float*)c.slabs);
   } else {
     hipLaunchKernelGGL((gram_kernel<T, W, GRAM_CROSS>), dim3(c.P, c.g.gchunks, XS),
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
@@ -2209,6 +2364,45 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
 // Test/diagnostic hook: X <- X Q for ONE column-block pair (blocks 0 and 1 of
 // X, 2W columns with leading dimension ld, rows padded to SVDJ_ROW_ALIGN),
 // Q row-major 2W x 2W on the device, with the given matrix-core mode.
+// Cross Gram alone (tests / kernel A/B): slabs (P x nchunk x W x W) of
+// A_bi^T A_bj for the device pair list, with the given row chunking.
+// kernel: 0 = register-fragment gram_kernel, 2..4 = LDS-staged with that
+// ring depth (fp32 W = 64).
+extern "C" int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int lda, int m_pad,
+                               const int32_t* pairs, int P, int rows_per_chunk, void* slabs,
+                               void* stream) {
+  if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad || P <= 0 || rows_per_chunk <= 0 ||
+      rows_per_chunk % SVDJ_ROW_ALIGN) {
+    set_error("svdj_gram_cross: bad m_pad/lda/P/rows %d/%d/%d/%d", m_pad, lda, P, rows_per_chunk);
+    return -2;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
+  if (kernel >= 2) {  // LDS-staged, ring depth `kernel`
+    if (dtype != 0 || W != 64 || lda % 4 || (uintptr_t)A % 16 || kernel > 4) {
+      set_error("svdj_gram_cross: LDS kernel needs fp32, W=64, 16-byte aligned columns, depth 2..4");
+      return -3;
+    }
+    launch_gram_lds(kernel, dim3(P, nchunk), st, (const float*)A, lda, m_pad, pairs, rows_per_chunk,
+                    (float*)slabs);
+  } else if (dtype == 0 && W == 64) {
+    hipLaunchKernelGGL((gram_kernel<float, 64, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
+                       0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
+  } else if (dtype == 0 && W == 32) {
+    hipLaunchKernelGGL((gram_kernel<float, 32, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
+                       0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
+  } else {
+    set_error("svdj_gram_cross: unsupported dtype=%d W=%d", dtype, W);
+    return -3;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("svdj_gram_cross launch: %s", hipGetErrorString(e));
+    return -101;
+  }
+  return 0;
+}
+
 extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q,
                             void* stream) {
   if (rows <= 0 || rows % SVDJ_ROW_ALIGN || ld < rows) {

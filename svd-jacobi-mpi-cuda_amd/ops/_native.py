@@ -123,6 +123,9 @@ def hip_lib():
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
               c_void_p])
+        _sig(lib, "svdj_gram_cross", c_int,
+             [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+              c_void_p])
         _sig(lib, "svdj_apply_q", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,

@@ -334,6 +334,23 @@ def block_steps_multi(At, Vt, D, m_pad, W, tol, max_inner, metric, chains, mma="
         _ptr(metric), mma_code(mma, At.dtype)), "block_steps_multi")
 
 
+def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int, rows_per_chunk: int,
+               kernel: str = "lds", depth: int = 4) -> torch.Tensor:
+    """Cross Gram A_bi^T A_bj of every (bi, bj) in ``pairs`` (P, 2) on the
+    device, split over row chunks as in a block step; returns the chunk slabs
+    (P, nchunk, W, W).  ``kernel``: "lds" (LDS-staged, fp32 W=64, ring of
+    ``depth`` stages) or "reg"."""
+    _check_layout(At, m_pad)
+    pairs = pairs.to(torch.int32).contiguous().to(At.device)
+    P = pairs.shape[0]
+    nchunk = -(-m_pad // rows_per_chunk)
+    slabs = torch.empty(P, nchunk, W, W, dtype=At.dtype, device=At.device)
+    hip_check(hip_lib().svdj_gram_cross(dtype_code(At.dtype), W, depth if kernel == "lds" else 0,
+                                        _ptr(At), At.stride(0), m_pad, _ptr(pairs), P,
+                                        rows_per_chunk, _ptr(slabs), _stream(At)), "gram_cross")
+    return slabs
+
+
 def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
     """Xt (2W, ld) rows = columns of X, in place X <- X Q (device tensors)."""
     _check_layout(Xt, Xt.shape[1] // ROW_ALIGN * ROW_ALIGN)
@@ -389,4 +406,5 @@ __all__ = [
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_steps2", "block_steps_multi", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",
+    "gram_cross",
 ]

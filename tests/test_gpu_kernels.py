@@ -358,3 +358,27 @@ def test_block_steps_multi_chain_matches_sequential(svdj, cuda):
     a0, v0, d0, m0 = run(False)
     assert m1[1] == m0[1] > 0
     assert torch.equal(a1, a0) and torch.equal(v1, v0) and torch.equal(d1, d0)
+
+
+@pytest.mark.parametrize("m,m_pad,rows", [(100, 128, 128), (500, 512, 128), (4000, 4096, 1024),
+                                          (5000, 5120, 3072), (3000, 3072, 256)])
+def test_gram_cross_lds_matches_reference(svdj, cuda, m, m_pad, rows):
+    """LDS-staged cross Gram (fp32 W=64, glds ring) vs the fp64 torch product
+    and vs the register-fragment kernel: 1 to 24 stages per chunk (ring
+    prologue / drain paths), a short last chunk, and a leading dimension
+    larger than m_pad."""
+    K = svdj.ops.kernels
+    W, nb = 64, 6
+    ld = m_pad + 128
+    At = torch.zeros(nb * W, ld, dtype=torch.float32, device=cuda)
+    At[:, :m_pad] = _rand_At(nb * W, m_pad, m, torch.float32, cuda, seed=5)
+    pairs = torch.tensor([[0, 5], [3, 1], [2, 4]], dtype=torch.int32)
+    reg = K.gram_cross(At, m_pad, pairs, W, rows, "reg").double().sum(1).cpu()
+    A64 = At.double().cpu()[:, :m_pad]
+    for depth in (2, 3, 4):
+        lds = K.gram_cross(At, m_pad, pairs, W, rows, "lds", depth).double().sum(1).cpu()
+        for p, (bi, bj) in enumerate(pairs.tolist()):
+            ref = A64[bi * W:(bi + 1) * W] @ A64[bj * W:(bj + 1) * W].t()
+            scale = ref.abs().max().item()
+            assert (lds[p] - ref).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
+            assert (lds[p] - reg[p]).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Where the time of a block-Jacobi kernel trace goes (dev aid).
+
+Splits the span of a rocprofv3 --kernel-trace SQLite database into the time
+during which (a) an apply or Gram kernel is running (the chip is doing the
+wide, GPU-filling work), (b) only EVD kernels run (one workgroup per pair:
+the chip is mostly idle), (c) nothing of ours runs.  (b)+(c) is the latency
+the two staggered chains fail to hide.
+
+    python tools/trace_crit.py run_results.db [more.db ...]
+"""
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def union(iv):
+    iv = sorted(iv)
+    out = []
+    for s, e in iv:
+        if out and s <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], e)
+        else:
+            out.append([s, e])
+    return out
+
+
+def length(iv):
+    return sum(e - s for s, e in iv)
+
+
+def minus(a, b):
+    """a \\ b for sorted disjoint interval lists."""
+    out, j = [], 0
+    for s, e in a:
+        cur = s
+        while j < len(b) and b[j][1] <= cur:
+            j += 1
+        k = j
+        while k < len(b) and b[k][0] < e:
+            if b[k][0] > cur:
+                out.append([cur, b[k][0]])
+            cur = max(cur, b[k][1])
+            k += 1
+        if cur < e:
+            out.append([cur, e])
+    return out
+
+
+def kind(name):
+    n = name.lower()
+    for k in ("gram", "evd", "apply"):
+        if k in n:
+            return k
+    return "other"
+
+
+def main(path):
+    db = sqlite3.connect(path)
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+    d = [dict(zip(cols, r)) for r in db.execute("select * from kernels")]
+    d = [x for x in d if "svdj" in x["name"]]
+    d.sort(key=lambda x: x["start"])
+    t0, t1 = d[0]["start"], max(x["end"] for x in d)
+    by = defaultdict(list)
+    for x in d:
+        by[kind(x["name"])].append((x["start"], x["end"]))
+    wide = union(by["gram"] + by["apply"] + by["other"])
+    evd = union(by["evd"])
+    span = t1 - t0
+    only_evd = length(minus(evd, wide))
+    busy = length(union(wide + evd))
+    print(f"{path}\n  span {span / 1e6:.2f} ms; wide (gram/apply) busy {length(wide) / 1e6:.2f} ms "
+          f"({100 * length(wide) / span:.1f} %), EVD-only {only_evd / 1e6:.2f} ms "
+          f"({100 * only_evd / span:.1f} %), idle {(span - busy) / 1e6:.2f} ms")
+    for k, iv in sorted(by.items()):
+        tot = sum(e - s for s, e in iv)
+        print(f"  {k:6s} n={len(iv):6d} sum {tot / 1e6:9.2f} ms avg {tot / len(iv) / 1e3:8.1f} us "
+              f"union {length(union(iv)) / 1e6:8.2f} ms")
+
+
+if __name__ == "__main__":
+    for p in sys.argv[1:]:
+        main(p)
