@@ -1145,6 +1145,276 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
 }
 
+// ------------------------------------------- evd, register-resident (bip)
+// The bipartite cross-step EVD (fp32 W = 64) with G held in REGISTERS in slot
+// space instead of LDS in position space.  The LDS kernel above is bound by
+// its G update: ~25 LDS instructions per thread and step at a 38 % bank
+// conflict share (profiles/r2_evd_unroll), and the EVD is the part of a step
+// the other chain cannot hide once a GPU holds few pairs
+// (tools/trace_crit.py: EVD-only time 2.6 % of a 1-GPU sweep, 24 % at 8 GPUs).
+//
+// Slot space: 2 x 2 blocks B(i, j) = [[G(X_i, X_j), G(X_i, Y_j)],
+// [G(Y_i, X_j), G(Y_i, Y_j)]], X_i column i of block bi (fixed), Y_j the
+// column of block bj at slot j in the current step (slot j pairs X_j with
+// Y_j; every step slot j+1's Y moves to slot j, Ord<W, EVD_BIP>).  The block
+// matrix is held by DIAGONAL: thread (wave w, lane l) holds B(l, l + d) for
+// d = 4w + r, r = 0..3 (16 fp32 registers), so
+//   * wave 0, r = 0 holds every diagonal block B(k, k): wave 0 alone solves
+//     the next step's 64 rotations, from registers (G(X_k, Y_{k+1}) is its
+//     r = 1 entry, G(Y_{k+1}, Y_{k+1}) one DPP lane away), no divergence;
+//   * a block's row rotation is the lane's slot (one record read), its column
+//     rotation slot l + d (four consecutive records);
+//   * the Y move is a register move along d for G(X, Y) (d + 1), a DPP lane
+//     rotate plus a register move for G(Y, X) (i + 1, d - 1) and a DPP lane
+//     rotate for G(Y, Y); the two register moves that cross a wave go through
+//     a 64-entry LDS exchange read after the next barrier.
+// The 2 x 2 updates run as packed fp32 (v_pk_fma_f32 on register pairs).
+// Q as in the LDS kernel's slot layout, fp64, 8 rows per thread on all waves.
+// ONE barrier per step; ~12 LDS instructions per thread and step (against
+// ~25), no bank conflicts.
+//
+// Same rotations, order, stop test, skip rule and outputs (Q, D, skip,
+// metric) as evd_kernel<float, 64, EVD_BIP>: tests/test_gpu_kernels.py checks
+// it against the fp64 reference with the bipartite ordering and against the
+// LDS kernel.
+//
+// Measured (profiles/r2_evdreg): correct, but SLOWER end to end (8-GPU rank
+// plan 66.4 -> 80.3 ms per sweep; a first row-major version that solved in
+// every wave 95.9).  It is VALU-issue bound: holding both triangles doubles
+// the G arithmetic the LDS kernel does on its packed triangle, the fp64 Q
+// rotation costs the same in both, and ~200 VALU instructions per wave and
+// step at four waves per SIMD exceed the LDS kernel's LDS-bound step.  Off by
+// default (SVDJ_EVD_REG=1 turns it on).
+#ifndef SVDJ_EVD_REG_DEFAULT
+#define SVDJ_EVD_REG_DEFAULT 0
+#endif
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+__global__ __launch_bounds__(1024) void evd_bip_reg_kernel(
+    const int32_t* __restrict__ pairs, const float* __restrict__ slabs, int nchunk,
+    float* __restrict__ D, float* __restrict__ Qout, int32_t* __restrict__ skip, float tol,
+    int absmode, int max_inner, uint32_t* __restrict__ metric) {
+  constexpr int W = 64, N = 2 * W, NT = 1024, NWAVE = NT / 64;
+  constexpr int RB = W / NWAVE;   // diagonals per thread (4)
+  constexpr int RQ = N / NWAVE;   // Q rows per thread (8)
+  using f2 = Pair2<float>;
+  using d2 = Pair2<double>;
+  __shared__ float Cs[W][W + 1];   // summed cross Gram
+  __shared__ float dg[N];          // diagonals, players X 0..W-1, Y W..2W-1
+  __shared__ f2 rcs[2][W], rdd[2][W];
+  __shared__ d2 rq[2][W];
+  __shared__ float xxy[2][NWAVE][W];  // every wave's d = 4w entry of G(X, Y) after the update
+  __shared__ float xyx[2][NWAVE][W];  // every wave's d = 4w+3 entry of G(Y, X)
+  __shared__ int rot_flag[2];
+  __shared__ float wmax[NWAVE];
+  __shared__ int wneed[NWAVE];
+  __shared__ int need_any;
+
+  const int pair = blockIdx.x;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- assemble: diagonals, cross Gram (split-K slabs summed in fp64), the
+  // convergence value and the "anything to rotate" pre-test
+  for (int a = tid; a < N; a += NT) dg[a] = D[a < W ? bi * W + a : bj * W + (a - W)];
+  __syncthreads();
+  {
+    float mx = 0.0f;
+    int need = 0;
+    const float* s0 = slabs + (size_t)pair * nchunk * (W * W);
+    for (int gi = tid; gi < W * W / 4; gi += NT) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 8
+      for (int c = 0; c < nchunk; ++c) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)c * W * W + gi * 4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += (double)v[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = gi * 4 + u, r = i / W, c = i % W;
+        const float g = (float)acc[u];
+        Cs[r][c] = g;
+        const float grr = dg[r], gcc = dg[W + c];
+        const float d = sqrtf(grr) * sqrtf(gcc);
+        if (d > 0.0f) {
+          const float v = fabsf(g) / d;
+          mx = v > mx ? v : mx;
+        }
+        need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
+      }
+    }
+    mx = wave_max(mx);
+    need = __any(need) ? 1 : 0;
+    if (lane == 0) {
+      wmax[wave] = mx;
+      wneed[wave] = need;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float m2 = 0.0f;
+      int n2 = 0;
+      for (int w = 0; w < NWAVE; ++w) {
+        m2 = wmax[w] > m2 ? wmax[w] : m2;
+        n2 |= wneed[w];
+      }
+      atomic_max_pos(&metric[0], m2);
+      need_any = n2;
+    }
+    __syncthreads();
+  }
+  const bool run = need_any != 0 && max_inner > 0;
+
+  // ---- registers: B(lane, lane + 4 wave + r) as two packed pairs per entry
+  // kind (r = 0, 1 and r = 2, 3); Q rows 8 wave + u
+  f32x2 xx[2], xy[2], yx[2], yy[2];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int d = RB * wave + r, j = (lane + d) & (W - 1);
+    xy[r >> 1][r & 1] = Cs[lane][j];
+    yx[r >> 1][r & 1] = Cs[j][lane];
+    xx[r >> 1][r & 1] = d == 0 ? dg[lane] : 0.0f;       // blocks are internally orthogonal
+    yy[r >> 1][r & 1] = d == 0 ? dg[W + lane] : 0.0f;
+  }
+  double qx[RQ], qy[RQ];
+#pragma unroll
+  for (int u = 0; u < RQ; ++u) {
+    const int k = RQ * wave + u;
+    qx[u] = k == lane ? 1.0 : 0.0;
+    qy[u] = k == W + lane ? 1.0 : 0.0;
+  }
+  const bool solver = wave == 0;  // slot k = lane, block B(k, k) in r = 0
+  float my_dp = 0.0f, my_dq = 0.0f, my_g = 0.0f;
+  bool my_rot = false;
+  auto publish = [&](int b, int k, float c, float s, float t, float dp, float dq) {
+    rcs[b][k] = f2{c, s};
+    rdd[b][k] = f2{dp, dq};
+    const double td = (double)t, c64 = rsqrt64(fma(td, td, 1.0));
+    rq[b][k] = d2{c64, td * c64};
+  };
+  int racc = 0, racc_next = 0;
+  if (run && solver) {  // step 0's rotations
+    const float gpp = xx[0][0], gqq = yy[0][0], gpq = xy[0][0];
+    float c, s, t;
+    my_rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
+    racc = my_rot;
+    my_g = gpq;
+    my_dp = gpp - t * gpq;
+    my_dq = gqq + t * gpq;
+    publish(0, lane, c, s, t, my_dp, my_dq);
+  }
+  __syncthreads();
+
+  bool any = false;
+  int gs = 0, sw = 0, st = 0;
+  const int wn = (wave + 1) & (NWAVE - 1), wp = (wave - 1) & (NWAVE - 1);
+  while (run) {
+    const int b = gs & 1, nb = b ^ 1;
+    const bool last = st + 1 == W;  // this phase solves step 0 of the next sweep
+    // deferred wave-crossing moves of the previous step
+    if (gs > 0) {
+      xy[1][1] = xxy[nb][wn][lane];                    // G(X_i, Y_{j+1}), d = 4w + 4
+      yx[0][0] = xyx[nb][wp][(lane + 1) & (W - 1)];    // G(Y_{i+1}, X_j), d = 4w - 1
+    }
+    // this step's rotations: row = slot `lane`, columns = slots lane + d
+    const f2 rr = rcs[b][lane];
+    f2 rcol[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) rcol[r] = rcs[b][(lane + RB * wave + r) & (W - 1)];
+    const d2 rqs = rq[b][lane];
+    // B <- R_i^T B R_j, packed over (r = 0, 1) and (r = 2, 3)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 ca = {rr.x, rr.x}, sa = {rr.y, rr.y};
+      const f32x2 cb = {rcol[2 * h].x, rcol[2 * h + 1].x};
+      const f32x2 sb = {rcol[2 * h].y, rcol[2 * h + 1].y};
+      const f32x2 h00 = ca * xx[h] - sa * yx[h], h01 = ca * xy[h] - sa * yy[h];
+      const f32x2 h10 = sa * xx[h] + ca * yx[h], h11 = sa * xy[h] + ca * yy[h];
+      xx[h] = cb * h00 - sb * h01;
+      xy[h] = sb * h00 + cb * h01;
+      yx[h] = cb * h10 - sb * h11;
+      yy[h] = sb * h10 + cb * h11;
+    }
+    if (solver) {  // the rotated pair's own block exactly: diag(d_p', d_q'), coupling 0
+      const float off = my_rot ? 0.0f : my_g;
+      xx[0][0] = my_dp;
+      yy[0][0] = my_dq;
+      xy[0][0] = off;
+      yx[0][0] = off;
+    }
+    xxy[b][wave][lane] = xy[0][0];
+    xyx[b][wave][lane] = yx[1][1];
+    // move to the next step's slots
+    //   G(X_i, Y_j)  <- d + 1           (r + 1; r = 3 from wave w+1 after the barrier)
+    //   G(Y_i, X_j)  <- i + 1, d - 1    (lane + 1, r - 1; r = 0 from wave w-1)
+    //   G(Y_i, Y_j)  <- i + 1           (lane + 1)
+    xy[0][0] = xy[0][1];
+    xy[0][1] = xy[1][0];
+    xy[1][0] = xy[1][1];
+    yx[1][1] = bip_shift<W>(yx[1][0], lane);
+    yx[1][0] = bip_shift<W>(yx[0][1], lane);
+    yx[0][1] = bip_shift<W>(yx[0][0], lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      yy[h][0] = bip_shift<W>(yy[h][0], lane);
+      yy[h][1] = bip_shift<W>(yy[h][1], lane);
+    }
+    if (solver) {  // the next step's rotation of slot `lane`
+      const float gpp = xx[0][0], gpq = xy[0][0], gqq = yy[0][0];
+      float c, s, t;
+      my_rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
+      if (last) racc_next |= my_rot; else racc |= my_rot;
+      my_g = gpq;
+      my_dp = gpp - t * gpq;
+      my_dq = gqq + t * gpq;
+      publish(nb, lane, c, s, t, my_dp, my_dq);
+      if (last) {  // every rotation of sweep sw is decided by now
+        const int rot = __any(racc) ? 1 : 0;
+        if (lane == 0) rot_flag[sw & 1] = rot;
+        racc = racc_next;
+        racc_next = 0;
+      }
+    }
+    // Q <- Q J (fp64), then the Y columns move with their players
+#pragma unroll
+    for (int u = 0; u < RQ; ++u) {
+      const double x = qx[u], y = qy[u];
+      qx[u] = rqs.x * x - rqs.y * y;
+      qy[u] = rqs.y * x + rqs.x * y;
+    }
+#pragma unroll
+    for (int u = 0; u < RQ; ++u) qy[u] = bip_shift<W>(qy[u], lane);
+    __syncthreads();
+    ++gs;
+    if (++st < W) continue;
+    st = 0;
+    if (!rot_flag[sw & 1]) break;
+    any = true;
+    if (++sw >= max_inner) break;
+  }
+
+  if (tid == 0) {
+    skip[pair] = any ? 0 : 1;
+    if (any) atomicAdd(&metric[1], 1u);
+  }
+  if (!any) return;  // cross mode: D only changes with a rotation
+  {
+    float* qo = Qout + (size_t)pair * N * N;
+    const int ps = W + ((lane + gs) & (W - 1));  // Y player now at slot `lane`
+#pragma unroll
+    for (int u = 0; u < RQ; ++u) {
+      const int k = RQ * wave + u;
+      qo[k * N + lane] = (float)qx[u];
+      qo[k * N + ps] = (float)qy[u];
+    }
+  }
+  if (tid < W) {  // diagonals after the last executed step (gs - 1)
+    const int lb = (gs - 1) & 1;
+    const int q = W + ((tid + gs - 1) & (W - 1));
+    D[bi * W + tid] = rdd[lb][tid].x;
+    D[bj * W + (q - W)] = rdd[lb][tid].y;
+  }
+}
+
 // ------------------------------------------------------------------ apply
 #ifndef SVDJ_APPLY_QPD
 #define SVDJ_APPLY_QPD 8
@@ -1728,6 +1998,22 @@ static bool gram_lds_ok(const Chain<T>& c) {
   }
 }
 
+// Register-resident bipartite EVD (fp32 W = 64): off by default (slower,
+// see evd_bip_reg_kernel), SVDJ_EVD_REG=1 selects it; svdj_set_evd_reg()
+// overrides both (tests run the two kernels in one process).
+static int g_evd_reg = -1;
+static bool evd_reg_enabled() {
+  static const bool env = [] {
+    const char* e = getenv("SVDJ_EVD_REG");
+    return e ? e[0] != '0' : SVDJ_EVD_REG_DEFAULT != 0;
+  }();
+  return g_evd_reg < 0 ? env : g_evd_reg != 0;
+}
+template <typename T, int W>
+static bool evd_reg_ok() {
+  return std::is_same<T, float>::value && W == 64 && evd_reg_enabled();
+}
+
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
 template <typename T, int W>
@@ -1753,7 +2039,11 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   }
   SVDJ_LAUNCH_CHECK();
-  if (mode == 2)
+  if (mode == 2 && evd_reg_ok<T, W>())
+    hipLaunchKernelGGL(evd_bip_reg_kernel, dim3(c.P), dim3(1024), 0, c.st, pr, (const float*)c.slabs,
+                       c.g.gchunks, (float*)c.D, (float*)c.Qb[b], c.skipb[b], (float)tol, absmode,
+                       max_inner, metric);
+  else if (mode == 2)
     hipLaunchKernelGGL((evd_kernel<T, W, EVD_BIP>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr,
                        0, c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode,
                        max_inner, metric);
@@ -2400,6 +2690,13 @@ extern "C" int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int 
     set_error("svdj_gram_cross launch: %s", hipGetErrorString(e));
     return -101;
   }
+  return 0;
+}
+
+// Select the bipartite EVD kernel for fp32 W = 64: 1 register-resident,
+// 0 LDS position-space, -1 back to the SVDJ_EVD_REG / build default.
+extern "C" int svdj_set_evd_reg(int on) {
+  g_evd_reg = on < 0 ? -1 : (on ? 1 : 0);
   return 0;
 }
 

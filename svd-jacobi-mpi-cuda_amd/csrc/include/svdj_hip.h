@@ -110,6 +110,7 @@ int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
 // Diagnostic hook: X <- X Q for one pair of column blocks (X = 2W columns,
 // leading dimension ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major
 // 2W x 2W on the device, with matrix-core mode `mma` (as svdj_block_steps).
+int svdj_set_evd_reg(int on);
 int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int lda, int m_pad,
                     const int32_t* pairs, int P, int rows_per_chunk, void* slabs, void* stream);
 int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q, void* stream);

@@ -123,6 +123,7 @@ def hip_lib():
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
               c_void_p])
+        _sig(lib, "svdj_set_evd_reg", c_int, [c_int])
         _sig(lib, "svdj_gram_cross", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
               c_void_p])

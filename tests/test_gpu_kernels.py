@@ -382,3 +382,56 @@ def test_gram_cross_lds_matches_reference(svdj, cuda, m, m_pad, rows):
             scale = ref.abs().max().item()
             assert (lds[p] - ref).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
             assert (lds[p] - reg[p]).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
+
+
+@pytest.mark.parametrize("inner,converged_pair", [(1, False), (3, False), (1, True)])
+def test_evd_register_kernel_matches_lds_kernel(svdj, cuda, inner, converged_pair):
+    """fp32 W=64 bipartite cross step: the register-resident EVD
+    (evd_bip_reg_kernel) against the LDS position-space EVD on the same input
+    -- one and several inner sweeps, and a pair that is already converged
+    (skipped exactly: same rotation count, D untouched)."""
+    K = svdj.ops.kernels
+    lib = svdj.ops.hip_lib()
+    W, nb, m, m_pad = 64, 4, 700, 768
+    g = torch.Generator().manual_seed(11)
+    A64 = torch.zeros(nb * W, m_pad, dtype=torch.float64)
+    if converged_pair:
+        q, _ = torch.linalg.qr(torch.rand(m, 2 * W, generator=g, dtype=torch.float64))
+        q = q * torch.linspace(1, 4, 2 * W, dtype=torch.float64)
+        A64[0:W, :m], A64[3 * W:4 * W, :m] = q[:, :W].t(), q[:, W:].t()
+        todo = (1, 2)
+    else:
+        todo = range(nb)
+    for b in todo:
+        qb, _ = torch.linalg.qr(torch.rand(m, W, generator=g, dtype=torch.float64))
+        A64[b * W:(b + 1) * W, :m] = (qb * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+    pairs = torch.tensor([[[0, 3], [1, 2]]], dtype=torch.int32, device=cuda)
+    out = {}
+    try:
+        for reg in (1, 0):
+            lib.svdj_set_evd_reg(reg)
+            At = A64.float().to(cuda)
+            Vt = torch.zeros(nb * W, 256, dtype=torch.float32, device=cuda)
+            K.set_identity(Vt, nb * W)
+            D = K.col_norms2(At, m_pad)
+            D0 = D.clone()
+            metric = K.new_metric(cuda)
+            K.block_steps(At, Vt, D, m_pad, pairs, W, [0], 1e-6, inner, metric,
+                          inner_order="bipartite")
+            out[reg] = (At.double().cpu(), Vt.double().cpu(), D.double().cpu(), D0.double().cpu(),
+                        K.read_metric(metric))
+    finally:
+        lib.svdj_set_evd_reg(-1)
+    (A1, V1, D1, D01, (mx1, n1)), (A0, V0, D0_, _, (mx0, n0)) = out[1], out[0]
+    assert n1 == n0 == (1 if converged_pair else 2)
+    assert math.isclose(mx1, mx0, rel_tol=1e-5)
+    # the LDS kernel keeps one copy of each symmetric entry, this one two
+    # (G(X_i, Y_j) and G(Y_j, X_i) rounded in different threads): rounding
+    # level apart after one sweep, drifting a little over several
+    tol = 2e-5 if inner == 1 else 1e-4
+    torch.testing.assert_close(A1, A0, rtol=tol, atol=tol)
+    torch.testing.assert_close(V1, V0, rtol=tol, atol=tol)
+    torch.testing.assert_close(D1, D0_, rtol=tol, atol=tol)
+    if converged_pair:
+        c03 = list(range(0, W)) + list(range(3 * W, 4 * W))
+        assert torch.equal(D1[c03], D01[c03])

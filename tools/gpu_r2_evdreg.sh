@@ -1,0 +1,20 @@
+#!/bin/bash
+# Register-resident bipartite EVD (fp32 W=64): kernel tests, then A/B against
+# the LDS EVD (SVDJ_EVD_REG=0) on the 1-GPU headline and the 8/2-GPU rank plans.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/evdreg
+mkdir -p $O
+export SVDJ_NO_AUTOBUILD=1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for v in ${VARIANTS:-1 0}; do
+  for P in 8 2; do
+    SVDJ_EVD_REG=$v timeout -k 10 300 python -u bench.py --simulate-P $P --simulate-rank 0 --n 16384 --sim-sweeps 2 \
+      --json-out $O/sim_p${P}_reg$v.json > $O/sim_p${P}_reg$v.log 2>&1 || { tail -20 $O/sim_p${P}_reg$v.log; exit 1; }
+    echo "reg=$v sim P=$P: $(python3 -c "import json; print(json.load(open('$O/sim_p${P}_reg$v.json'))['value'])") ms/sweep"
+  done
+  SVDJ_EVD_REG=$v timeout -k 10 300 python -u bench.py --n 16384 --steps 1 --warmup 1 --json-out $O/one_reg$v.json \
+    > $O/one_reg$v.log 2>&1 || { tail -20 $O/one_reg$v.log; exit 1; }
+  echo "reg=$v 1-GPU 16384: $(python3 -c "import json; d=json.load(open('$O/one_reg$v.json')); print(d['ms_per_step'], 'ms', d['sweeps'], d['accuracy'])")"
+done

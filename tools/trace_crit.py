@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where the time of a block-Jacobi kernel trace goes (dev aid).
 
-Splits the span of a rocprofv3 --kernel-trace SQLite database into the time
+Splits the span of the last solve in a rocprofv3 --kernel-trace SQLite database
 during which (a) an apply or Gram kernel is running (the chip is doing the
 wide, GPU-filling work), (b) only EVD kernels run (one workgroup per pair:
 the chip is mostly idle), (c) nothing of ours runs.  (b)+(c) is the latency
@@ -55,12 +55,19 @@ def kind(name):
     return "other"
 
 
-def main(path):
+def main(path, last_solve=True):
     db = sqlite3.connect(path)
     cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
     d = [dict(zip(cols, r)) for r in db.execute("select * from kernels")]
     d = [x for x in d if "svdj" in x["name"]]
     d.sort(key=lambda x: x["start"])
+    if last_solve:  # keep what follows the longest gap between our kernels
+        ends, mx = [], 0
+        for x in d:
+            mx = max(mx, x["end"])
+            ends.append(mx)
+        cut = max(range(1, len(d)), key=lambda i: d[i]["start"] - ends[i - 1])
+        d = d[cut:]
     t0, t1 = d[0]["start"], max(x["end"] for x in d)
     by = defaultdict(list)
     for x in d:
@@ -70,13 +77,20 @@ def main(path):
     span = t1 - t0
     only_evd = length(minus(evd, wide))
     busy = length(union(wide + evd))
-    print(f"{path}\n  span {span / 1e6:.2f} ms; wide (gram/apply) busy {length(wide) / 1e6:.2f} ms "
+    gaps = sorted(minus([[t0, t1]], union(wide + evd)), key=lambda g: g[0] - g[1])
+    print(f"{path}\n  {len(d)} kernels; span {span / 1e6:.2f} ms; wide (gram/apply) busy {length(wide) / 1e6:.2f} ms "
           f"({100 * length(wide) / span:.1f} %), EVD-only {only_evd / 1e6:.2f} ms "
           f"({100 * only_evd / span:.1f} %), idle {(span - busy) / 1e6:.2f} ms")
     for k, iv in sorted(by.items()):
         tot = sum(e - s for s, e in iv)
         print(f"  {k:6s} n={len(iv):6d} sum {tot / 1e6:9.2f} ms avg {tot / len(iv) / 1e3:8.1f} us "
               f"union {length(union(iv)) / 1e6:8.2f} ms")
+    hist = defaultdict(float)
+    for s, e in gaps:
+        us = (e - s) / 1e3
+        hist[next(b for b in (5, 10, 20, 50, 100, 1e12) if us < b)] += us / 1e3
+    print("  idle ms by gap length (us): " + ", ".join(
+        f"<{b:g}: {v:.2f}" for b, v in sorted(hist.items())))
 
 
 if __name__ == "__main__":
