@@ -22,6 +22,7 @@
 // are the tracked squared column norms D.  The first step of a sweep uses the
 // full Gram, which re-measures every within-block angle from the data.
 #include "common.hpp"
+#include "evd_deal_tables.hpp"
 #include "svdj_hip.h"
 
 #include <cstdlib>
@@ -682,12 +683,25 @@ __host__ __device__ constexpr int block_duty_o(int a, int b) {  // 256*e + meeti
 // in complementary pairs 0, W-2, 1, W-3, ... (two paired rows hold W blocks,
 // so a wave's lanes share few slots and the record reads broadcast).
 // blk[j * NT + t] = (a << 8) | b of thread t's j-th block, 0xffff if none.
-template <int W, int NT, int ORD = EVD_CYCLIC>
+// OPT (fp32, bipartite, 1024 threads): the table of tools/evd_deal_opt.py
+// instead -- the same duty blocks, the other blocks placed so the 32 lanes of
+// each LDS lane group hit distinct banks where possible (modelled LDS cycles
+// per step W=64: 1144 -> 812, conflict share 45 -> 22 %).
+#ifndef SVDJ_EVD_DEAL_OPT
+#define SVDJ_EVD_DEAL_OPT 1
+#endif
+template <int W, int NT, int ORD = EVD_CYCLIC, bool OPT = false>
 struct EvdDeal {
   static constexpr int NOFF = W * (W - 1) / 2;
   static constexpr int MAXOFF = (NOFF + NT - 1) / NT;
   unsigned short blk[MAXOFF * NT];
   constexpr EvdDeal() : blk{} {
+    if constexpr (OPT) {
+      static_assert(ORD == EVD_BIP && NT == 1024 && (W == 32 || W == 64), "optimised dealing tables");
+      const unsigned short* t = W == 64 ? kEvdDealF32_W64_bip : kEvdDealF32_W32_bip;
+      for (int g = 0; g < MAXOFF * NT; ++g) blk[g] = t[g];
+      return;
+    }
     using O = Ord<W, ORD>;
     int g = 0;
     // duty block of each next-step slot s: the positions that slot's players
@@ -712,12 +726,12 @@ struct EvdDeal {
 
 // Compile-time check of the dealing: the first W entries are the duty blocks
 // of next-step slots 0..W-1, and every block is dealt exactly once.
-template <int W, int NT, int ORD>
+template <int W, int NT, int ORD, bool OPT = false>
 constexpr bool evd_deal_ok() {
-  constexpr EvdDeal<W, NT, ORD> d{};
+  constexpr EvdDeal<W, NT, ORD, OPT> d{};
   int seen[W * W] = {};
   int dealt = 0;
-  for (int g = 0; g < EvdDeal<W, NT, ORD>::MAXOFF * NT; ++g) {
+  for (int g = 0; g < EvdDeal<W, NT, ORD, OPT>::MAXOFF * NT; ++g) {
     if (d.blk[g] == 0xffff) continue;
     const int a = d.blk[g] >> 8, b = d.blk[g] & 255;
     if (!(a < b && b < W) || seen[a * W + b]++) return false;
@@ -726,12 +740,19 @@ constexpr bool evd_deal_ok() {
     if (g < W && (duty < 0 || ((duty & 255) >> 1) != g)) return false;
     if (g >= W && duty >= 0) return false;
   }
-  return dealt == EvdDeal<W, NT, ORD>::NOFF;
+  return dealt == EvdDeal<W, NT, ORD, OPT>::NOFF;
 }
 static_assert(evd_deal_ok<32, evd_threads(32), EVD_CYCLIC>(), "EVD block dealing");
 static_assert(evd_deal_ok<64, evd_threads(64), EVD_CYCLIC>(), "EVD block dealing");
 static_assert(evd_deal_ok<32, evd_threads(32), EVD_BIP>(), "EVD block dealing");
 static_assert(evd_deal_ok<64, evd_threads(64), EVD_BIP>(), "EVD block dealing");
+static_assert(evd_deal_ok<64, 1024, EVD_BIP, true>(), "optimised EVD block dealing");
+static_assert(evd_deal_ok<32, 1024, EVD_BIP, true>(), "optimised EVD block dealing");
+// which dealing a kernel uses
+template <typename T, int W, int NT, int ORD>
+__host__ __device__ constexpr bool evd_deal_opt() {
+  return SVDJ_EVD_DEAL_OPT && sizeof(T) == 4 && ORD == EVD_BIP && NT == 1024 && (W == 32 || W == 64);
+}
 
 template <typename T, int W, int ORD>
 __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
@@ -754,14 +775,15 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   constexpr int QW0 = SVDJ_EVD_QALL ? 0 : 1;  // first Q wave
   constexpr int NGRP = (NWAVE - QW0) * GPW;
   constexpr int RPL = (N + NGRP - 1) / NGRP;  // Q rows per lane (the last group may idle)
-  constexpr int MAXOFF = EvdDeal<W, NT, ORD>::MAXOFF;
+  constexpr bool DOPT = evd_deal_opt<T, W, NT, ORD>();
+  constexpr int MAXOFF = EvdDeal<W, NT, ORD, DOPT>::MAXOFF;
   static_assert(W >= 4 && W <= 64 && NWAVE >= 2, "EVD geometry");
 #ifdef SVDJ_EVD_Q32
   using QT = T;
 #else
   using QT = double;
 #endif
-  static constexpr EvdDeal<W, NT, ORD> deal{};
+  static constexpr EvdDeal<W, NT, ORD, DOPT> deal{};
 
   __shared__ T Gb[2][NTRI + 1];  // off-diagonal G by position pair, double-buffered;
                                  // element NTRI takes the writes that go nowhere
