@@ -458,3 +458,44 @@ def test_bip_position_space_emulation(W):
     for a in range(W):
         p, q = _bip_players(W, a, R - 1)
         np.testing.assert_allclose([rec[lb][a][2], rec[lb][a][3]], [G[p, p], G[q, q]], rtol=1e-12)
+
+
+def _deal_tool():
+    import importlib.util
+    import os
+    p = os.path.join(os.path.dirname(__file__), "..", "tools", "evd_deal_opt.py")
+    spec = importlib.util.spec_from_file_location("evd_deal_opt", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _header_table(name):
+    import os
+    import re
+    p = os.path.join(os.path.dirname(__file__), "..", "svd-jacobi-mpi-cuda_amd", "csrc", "hip",
+                     "evd_deal_tables.hpp")
+    txt = open(p).read()
+    body = re.search(name + r"\[\d+\] = \{(.*?)\};", txt, re.S).group(1)
+    return [int(x, 16) for x in re.findall(r"0x[0-9a-f]{4}", body)]
+
+
+@pytest.mark.parametrize("W", [32, 64])
+def test_evd_deal_table_valid_and_cheaper(W):
+    """The generated fp32 bipartite EVD dealing (csrc/hip/evd_deal_tables.hpp,
+    tools/evd_deal_opt.py): duty blocks of next-step slots 0..W-1 first, every
+    slot-pair block exactly once, and fewer modelled LDS cycles per step than
+    the round-2 dealing (PMC: bank-conflict share 40 -> 20 %, profiles/r2_deal)."""
+    T = _deal_tool()
+    vals = _header_table(f"kEvdDealF32_W{W}_bip")
+    NT = T.NT
+    duty, rest = T.round2_deal(W, T.BIP)
+    blks = [None if v == 0xffff else (v >> 8, v & 255) for v in vals]
+    assert blks[:W] == duty
+    dealt = [b for b in blks if b is not None]
+    assert sorted(dealt) == sorted(duty + rest) and len(set(dealt)) == W * (W - 1) // 2
+    maxoff = len(vals) // NT
+    slots = [[blks[j * NT + t] for t in range(NT)] for j in range(maxoff)]
+    c_opt, _ = T.deal_cost(W, T.BIP, slots)
+    c_r2, _ = T.deal_cost(W, T.BIP, T.slots_from(duty, rest, W))
+    assert c_opt < 0.8 * c_r2, (c_opt, c_r2)
