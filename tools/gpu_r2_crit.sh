@@ -8,7 +8,7 @@ O=$R/gpurun_out/crit
 mkdir -p $O
 export SVDJ_NO_AUTOBUILD=1
 cd /tmp && export TMPDIR=/tmp
-for cfg in ${CFGS:-1:64 2:64 4:64 8:64}; do   # P:W
+for cfg in ${CFGS:-8:64}; do   # P:W
   set -- ${cfg/:/ }
   timeout -k 10 300 rocprofv3 --kernel-trace -d $O/p$1_w$2 -o run -- python $R/bench.py --simulate-P $1 \
     --simulate-rank 0 --n ${N:-16384} --sim-sweeps 2 --block $2 > $O/p$1_w$2.log 2>&1 || { tail -20 $O/p$1_w$2.log; exit 1; }

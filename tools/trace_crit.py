@@ -49,6 +49,8 @@ def minus(a, b):
 
 def kind(name):
     n = name.lower()
+    if "svdj" not in n:
+        return "torch"   # copies (simulated exchanges, copy-in), generator, norms
     for k in ("gram", "evd", "apply"):
         if k in n:
             return k
@@ -59,9 +61,8 @@ def main(path, last_solve=True):
     db = sqlite3.connect(path)
     cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
     d = [dict(zip(cols, r)) for r in db.execute("select * from kernels")]
-    d = [x for x in d if "svdj" in x["name"]]
     d.sort(key=lambda x: x["start"])
-    if last_solve:  # keep what follows the longest gap between our kernels
+    if last_solve:  # keep what follows the longest gap between kernels
         ends, mx = [], 0
         for x in d:
             mx = max(mx, x["end"])
@@ -72,7 +73,7 @@ def main(path, last_solve=True):
     by = defaultdict(list)
     for x in d:
         by[kind(x["name"])].append((x["start"], x["end"]))
-    wide = union(by["gram"] + by["apply"] + by["other"])
+    wide = union(by["gram"] + by["apply"] + by["other"] + by["torch"])
     evd = union(by["evd"])
     span = t1 - t0
     only_evd = length(minus(evd, wide))
@@ -85,12 +86,30 @@ def main(path, last_solve=True):
         tot = sum(e - s for s, e in iv)
         print(f"  {k:6s} n={len(iv):6d} sum {tot / 1e6:9.2f} ms avg {tot / len(iv) / 1e3:8.1f} us "
               f"union {length(union(iv)) / 1e6:8.2f} ms")
+    # launch-to-start delay per kernel kind: start minus the end of the
+    # previous kernel on the same stream (dependency + dispatch latency)
+    prev_end, delay = {}, defaultdict(list)
+    for x in d:
+        sid = x.get("stream_id", x.get("queue_id"))
+        if sid in prev_end:
+            delay[kind(x["name"])].append(max(0, x["start"] - prev_end[sid]) / 1e3)
+        prev_end[sid] = x["end"]
+    for k, v in sorted(delay.items()):
+        v = sorted(v)
+        print(f"  {k:6s} start delay after the stream's previous kernel: median {v[len(v) // 2]:.1f} us, "
+              f"p90 {v[int(len(v) * 0.9)]:.1f} us, sum {sum(v) / 1e3:.2f} ms")
     hist = defaultdict(float)
     for s, e in gaps:
         us = (e - s) / 1e3
         hist[next(b for b in (5, 10, 20, 50, 100, 1e12) if us < b)] += us / 1e3
     print("  idle ms by gap length (us): " + ", ".join(
         f"<{b:g}: {v:.2f}" for b, v in sorted(hist.items())))
+    big = sorted(gaps, key=lambda g: g[0] - g[1])[:6]
+    for gs_, ge in big:
+        before = max((x for x in d if x["end"] <= gs_), key=lambda x: x["end"])
+        after = min((x for x in d if x["start"] >= ge), key=lambda x: x["start"])
+        print(f"    gap {(ge - gs_) / 1e3:8.1f} us at {(gs_ - t0) / 1e6:8.2f} ms: after "
+              f"{kind(before['name'])} -> before {kind(after['name'])} {after['name'][:50]}")
 
 
 if __name__ == "__main__":
