@@ -80,6 +80,13 @@ class Communicator:
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
                 kw["device_id"] = self.device
+                # Create torch's stream pool (the solver's chain and comm
+                # streams come from it) BEFORE RCCL creates its own streams:
+                # HIP binds streams to the GPU_MAX_HW_QUEUES hardware queues
+                # in creation order, and two chain streams on one queue run
+                # serialised (profiles/r2_native_dist: the native driver
+                # measured exactly that until it created its streams first).
+                torch.cuda.Stream(self.device)
             dist.init_process_group(backend=backend,
                                     timeout=datetime.timedelta(seconds=self.timeout_s), **kw)
             self.owns_group = True
