@@ -72,6 +72,8 @@ def verify_distributed(res, gen, m, n, comm, dtype):
                          (U.t() @ U - eye).double().pow(2).sum()])
     if comm.distributed:
         import torch.distributed as dist
+        if dist.get_backend() == "gloo":  # host process group (--engine native)
+            parts = parts.cpu()
         dist.all_reduce(parts)
     parts = parts.cpu()
     return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
@@ -211,6 +213,168 @@ def simulate(a, cfg, dtype, work):
             json.dump(line, f)
 
 
+class _HostComm:
+    """world / distributed / rank of the gloo host group of --engine native."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    distributed = property(lambda self: self.world > 1)
+
+
+def run_native(a, dtype, work):
+    """--engine native: the C++ distributed solver (libsvdj_dist.so,
+    csrc/dist/svdj_dist.cpp) inside the bench process -- the same tournament,
+    half-exchange pipeline and block kernels as the Python executor, with the
+    sweep issued from C++ (RCCL ncclSend/ncclRecv on its own comm stream,
+    HIP events for every dependency).  torch.distributed runs on gloo here,
+    for the host-side barriers and the max over ranks only."""
+    import ctypes as C
+    import datetime
+
+    import torch.distributed as dist
+
+    import svdj
+    from svdj.ops import _native as NAT
+    from svdj.ops import kernels as K
+    from svdj.parallel.comm import default_timeout_s, env_world
+    from svdj.utils.metrics import algorithmic_flops_per_sweep, default_tol
+
+    rank, world, local = env_world()
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if dtype not in (torch.float32, torch.float64):
+        raise SystemExit("--engine native: fp32 or fp64")
+    shared = os.environ.get("SVDJ_SHARED_GPU") == "1"
+    dev = torch.device("cuda", 0 if shared else local)
+    torch.cuda.set_device(dev)
+    # the solver's streams first: HIP binds streams to hardware queues in
+    # creation order, RCCL creates its own at communicator init
+    sa, sb, sc = (torch.cuda.Stream(dev) for _ in range(3))
+    timeout = a.comm_timeout or default_timeout_s()
+    if shared:
+        os.environ["NCCL_HOSTID"] = f"svdj-shared-gpu-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout))
+    comm = _HostComm(rank, world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    lib = NAT.dist_lib()
+
+    def check(rc, what):
+        if rc < 0:
+            raise RuntimeError(f"{what}: {lib.svdj_dist_last_error().decode()}")
+
+    def say(msg):
+        if a.progress:
+            print(f"[bench native rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    id_path = f"/tmp/svdj_bench_{os.environ.get('MASTER_PORT', '0')}_{world}.id"
+    if rank == 0 and os.path.exists(id_path):
+        os.remove(id_path)
+    barrier()
+    nccl = C.c_void_p()
+    say(f"RCCL init via {id_path}")
+    check(lib.svdj_dist_comm_init(rank, world, id_path.encode(), float(timeout), C.byref(nccl)),
+          "svdj_dist_comm_init")
+    n = a.n
+    m = a.m or n
+    dcode = 1 if dtype == torch.float64 else 0
+    W = a.block or lib.svdj_dist_choose_block(dcode, world, m, n)
+    geo = [C.c_int32() for _ in range(4)]
+    check(lib.svdj_dist_geometry(world, m, n, W, *[C.byref(g) for g in geo]), "svdj_dist_geometry")
+    B, ncols, m_pad, n_v = (g.value for g in geo)
+    held0 = (C.c_int32 * 2)()
+    check(lib.svdj_dist_initial_held(world, rank, held0), "svdj_dist_initial_held")
+    At = torch.zeros(2 * B, m_pad, dtype=dtype, device=dev)
+    Vt = torch.zeros(2 * B, n_v, dtype=dtype, device=dev)
+    D = torch.empty(2 * B, dtype=dtype, device=dev)
+    S = torch.empty(2 * B, dtype=dtype, device=dev)
+    gen = make_generator(m, dev, work, dtype)
+    hist = (C.c_double * a.max_sweeps)()
+    p = NAT.DistProblem()
+    p.rank, p.world, p.comm, p.dtype = rank, world, nccl, dcode
+    p.W, p.m_pad, p.n_v, p.B = W, m_pad, n_v, B
+    p.At, p.Vt, p.D = At.data_ptr(), Vt.data_ptr(), D.data_ptr()
+    p.tol = a.tol if a.tol is not None else default_tol(dtype, m)
+    p.tol_mode, p.max_sweeps, p.mma = 0, a.max_sweeps, 0
+    p.inner_order = 1 if a.inner_order == "bipartite" else 0
+    p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
+    p.hist = C.cast(hist, C.POINTER(C.c_double))
+
+    def one():  # input generation (this rank's columns), V = I, norms, sweeps, U / sigma
+        with torch.cuda.stream(sa):
+            At.zero_()
+            for s_ in range(2):
+                c0 = held0[s_] * B
+                c1 = min(c0 + B, n)
+                if c1 > c0:
+                    At[s_ * B:s_ * B + (c1 - c0), :m] = gen(c0, c1).t()
+                K.set_identity(Vt[s_ * B:(s_ + 1) * B], B, c0)
+            K.col_norms2(At, m_pad, out=D)
+        p.held[0], p.held[1] = held0[0], held0[1]
+        say(f"solve (W={W}, B={B}, m_pad={m_pad}, n_v={n_v})")
+        check(lib.svdj_dist_solve(C.byref(p), C.c_void_p(S.data_ptr())), "svdj_dist_solve")
+        return p.sweeps, bool(p.converged)
+
+    for _ in range(a.warmup):
+        one()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sweeps, conv = [], True
+    for _ in range(a.steps):
+        sw, cv = one()
+        sweeps.append(sw)
+        conv = conv and cv
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    flops = sum(algorithmic_flops_per_sweep(m, n) * s_ for s_ in sweeps)
+    acc = None
+    if not a.no_verify:
+        class _Res:
+            pass
+        res = _Res()
+        res.U, res.V, res.S = At, Vt, S
+        res.info = {"geometry": {"B": B}, "held": [int(p.held[0]), int(p.held[1])]}
+        acc = verify_distributed(res, gen, m, n, comm, work)
+    if rank == 0:
+        ms = el / a.steps * 1e3
+        line = {
+            "metric": BASELINE_METRIC, "value": round(flops / el / 1e9, 2), "unit": "GFLOP/s",
+            "n_gpus": a.gpus, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic random dense U(0,1), seeded per column block; generated on the fly per rank",
+            "config": {"model": f"{m}x{n} {a.dtype} block one-sided Jacobi SVD (AllVec), to convergence",
+                       "global_batch": 1, "seq_len": n,
+                       "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
+                       "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
+                       "mma": "native", "precondition": "none", "chains": 2,
+                       "inner_order": a.inner_order, "staggered": True, "root_owned": False},
+            "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
+            "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
+            "accuracy": acc,
+        }
+        print(json.dumps(line), flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(line, f)
+    lib.svdj_dist_comm_destroy(nccl)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def svdj_default_inner() -> str:
     import svdj
     return svdj.SolverConfig().inner_order
@@ -249,6 +413,9 @@ def main():
     p.add_argument("--sim-sweeps", type=int, default=3)
     p.add_argument("--sim-link-gbps", type=float, default=0.0,
                    help="model each exchange's link time at this GB/s (0: device copy only)")
+    p.add_argument("--engine", default="python", choices=["python", "native"],
+                   help="distributed executor: torch.distributed + Python issue (python), or "
+                        "the C++ solver libsvdj_dist with RCCL called directly (native)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--no-verify", action="store_true",
                    help="skip the post-timing accuracy check")
@@ -270,6 +437,9 @@ def main():
         raise SystemExit("bench.py needs a GPU")
     if a.simulate_P:
         simulate(a, cfg, dtype, work)
+        return
+    if a.engine == "native":
+        run_native(a, dtype, work)
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -18,6 +18,7 @@ _LIBDIR = _PKG / "lib"
 _lock = threading.Lock()
 _cpu = None
 _hip = None
+_dist = None
 
 c_int = C.c_int
 c_double = C.c_double
@@ -136,6 +137,49 @@ def hip_lib():
              [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p])
         _sig(lib, "svdj_spin_ns", c_int, [c_double, c_void_p])
         _hip = lib
+        return lib
+
+
+class DistProblem(C.Structure):
+    """svdj_dist_problem (csrc/include/svdj_dist.h), field for field."""
+    _fields_ = [("rank", c_int), ("world", c_int), ("comm", c_void_p), ("dtype", c_int),
+                ("W", c_int), ("m_pad", c_int), ("n_v", c_int), ("B", c_int),
+                ("At", c_void_p), ("Vt", c_void_p), ("D", c_void_p), ("held", C.c_int32 * 2),
+                ("tol", c_double), ("tol_mode", c_int), ("max_sweeps", c_int), ("mma", c_int),
+                ("inner_order", c_int), ("stream_a", c_void_p), ("stream_b", c_void_p),
+                ("stream_comm", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
+                ("converged", c_int)]
+
+
+def dist_lib():
+    """Native distributed solver (libsvdj_dist.so: RCCL tournament over the
+    HIP block kernels, no Python in the sweep).  Loaded after torch, so its
+    librccl.so.1 / libamdhip64 resolve to the runtime torch already loaded."""
+    global _dist
+    if _dist is not None:
+        return _dist
+    hip_lib()  # (takes _lock itself)
+    with _lock:
+        if _dist is not None:
+            return _dist
+        from .. import _build
+
+        path = _build.DIST_LIB
+        if os.environ.get("SVDJ_NO_AUTOBUILD") != "1":
+            path = _build.build_dist()
+        if not path.exists():
+            raise NativeError(f"{path} missing")
+        lib = C.CDLL(str(path))
+        _sig(lib, "svdj_dist_comm_init", c_int,
+             [c_int, c_int, C.c_char_p, c_double, C.POINTER(c_void_p)])
+        _sig(lib, "svdj_dist_comm_destroy", c_int, [c_void_p])
+        _sig(lib, "svdj_dist_geometry", c_int,
+             [c_int, c_int, c_int, c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
+        _sig(lib, "svdj_dist_choose_block", c_int, [c_int, c_int, c_int, c_int])
+        _sig(lib, "svdj_dist_initial_held", c_int, [c_int, c_int, c_i32_p])
+        _sig(lib, "svdj_dist_solve", c_int, [C.POINTER(DistProblem), c_void_p])
+        _sig(lib, "svdj_dist_last_error", C.c_char_p, [])
+        _dist = lib
         return lib
 
 
