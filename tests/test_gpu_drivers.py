@@ -1,5 +1,6 @@
 """GPU end-to-end: native driver, CLI driver, distributed solver at world 1,
 determinism, checkpoint on device (needs MI355X)."""
+import json
 import os
 import subprocess
 import sys
@@ -95,3 +96,25 @@ def test_qr_preconditioned_fp32_gpu(svdj, cuda):
     for r in (res, plain):
         rep = svdj.utils.metrics.verify(A, r.U, r.S, r.V, ref)
         assert r.converged and rep["residual_rel"] < 1e-4 and rep["sigma_max_abs_err_over_smax"] < 1e-5, rep
+
+
+def test_bench_native_engine_matches_python_engine(tmp_path):
+    """bench.py --engine native (libsvdj_dist in the bench process, RCCL
+    world 1) runs the same solve as the Python executor: same sweeps, same
+    accuracy figures, bench JSON contract fields present."""
+    out = {}
+    for eng in ("native", "python"):
+        js = tmp_path / f"{eng}.json"
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--engine", eng,
+                            "--size", "1024", "--steps", "1", "--warmup", "0", "--json-out", str(js)],
+                           capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, MASTER_PORT=str(29950 + len(out))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[eng] = json.loads(js.read_text())
+    nat, py = out["native"], out["python"]
+    for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "config", "sweeps"):
+        assert k in nat
+    assert nat["config"]["engine"].startswith("native")
+    assert nat["sweeps"] == py["sweeps"] and nat["converged"]
+    assert nat["accuracy"]["residual_rel"] < 1e-5
+    assert abs(nat["accuracy"]["residual_rel"] - py["accuracy"]["residual_rel"]) < 1e-9
