@@ -1455,6 +1455,12 @@ __global__ __launch_bounds__(1024) void evd_bip_reg_kernel(
 #ifndef SVDJ_APPLY_QFRAG
 #define SVDJ_APPLY_QFRAG 2
 #endif
+// Row-layout Q fill: 0 element-wise (default), 1 16-byte copies.  The
+// 16-byte fill measured slower: 16384^2 rank plans P=2/4/8 206.5/125.5/62.7
+// -> 215.1/130.9/64.9 ms per sweep, 1 GPU 5.75 -> 5.79 s (tools/gpu_r2_q16*.sh)
+#ifndef SVDJ_APPLY_Q16
+#define SVDJ_APPLY_Q16 0
+#endif
 template <typename T, int W>
 __host__ __device__ constexpr int apply_threads() {
   return (W == 64 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_64
@@ -1542,11 +1548,13 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
         Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = q[u];
       }
     }
-  } else {
+  } else if constexpr (SVDJ_APPLY_Q16) {
     for (int iv = threadIdx.x; iv < N * N / VEC; iv += NTH) {
       const int i = iv * VEC;  // VEC consecutive columns of one row (N % VEC == 0)
       *reinterpret_cast<QV*>(&Qs[(i / N) * LDQ + (i % N)]) = Qgv[iv];
     }
+  } else {  // element-wise fill (A/B variant)
+    for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
   }
   __syncthreads();
   if (r0 >= r_end) return;
