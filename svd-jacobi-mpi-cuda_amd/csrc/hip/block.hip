@@ -1907,7 +1907,7 @@ struct Geometry {
   int a_chunks, rows_a, v_chunks, rows_v;
 };
 
-static Geometry make_geometry(int W, int P, int m_pad, int n_v) {
+static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   Geometry g;
   // Gram: split-K over row chunks (>= 128 rows each), ~512 workgroups.
   // Many pairs per step want few chunks (every chunk is a slab the EVD sums:
@@ -1926,12 +1926,22 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v) {
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.grows = round_up((m_pad + g.gchunks - 1) / g.gchunks, 128);
   g.gchunks = (m_pad + g.grows - 1) / g.grows;
-  // Apply: ~1024+ workgroups over A and V rows, >= 128 rows each.
+  // Apply: workgroups over A and V rows (128..2048 rows each, every one
+  // fills the pair's 2W x 2W Q into LDS first).  ~2048 workgroups for W = 32
+  // and for steps with >= 64 pairs (one GPU: 16384^2 5.79 s vs 5.87 s at
+  // 512); ~512 for W = 64 with fewer pairs, where the 64 KB Q fill of short
+  // workgroups costs more than the occupancy gains: 16384^2 rank plans
+  // P=2/4/8 206.5/126.2/63.0 -> 203.5/114.5/59.8 ms per sweep, 8192^2 one GPU
+  // 866 -> 799 ms, 32768x8192 (QR) 943 -> 888 ms; W = 32 (4096^2, fp64
+  // 5000^2) 2-3.5 % slower at 512 (tools/gpu_r2_awg2.sh / awg3.sh,
+  // profiles/r2_awg).  The split-bf16 applies (mma != 0) keep 2048: their
+  // larger Q images (32768x8192 bf16 with QR: 811 -> 847 ms at 512).
   int total_rows = m_pad + n_v;
-  static const int wg_target = [] {
+  static const int wg_env = [] {
     const char* e = getenv("SVDJ_APPLY_WG_TARGET");  // tuning experiments only
-    return e && atoi(e) > 0 ? atoi(e) : 2048;
+    return e && atoi(e) > 0 ? atoi(e) : 0;
   }();
+  const int wg_target = wg_env ? wg_env : (W == 64 && P < 64 && mma == 0 ? 512 : 2048);
   int rows = round_up((int)(((long)total_rows * P + wg_target - 1) / wg_target), 128);
   if (rows < 128) rows = 128;
   if (rows > 2048) rows = 2048;
@@ -1980,7 +1990,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   }
   c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
   c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
-  c.g = make_geometry(W, P, m_pad, V ? n_v : 0);
+  c.g = make_geometry(W, P, m_pad, V ? n_v : 0, mma);
   char* w = (char*)ws;
   c.slabs = (T*)w;
   w += ((size_t)P * c.g.gchunks * 4 * W * W * sizeof(T) + 255) / 256 * 256;
