@@ -379,6 +379,14 @@ struct alignas(2 * sizeof(T)) Pair2 {
 #ifndef SVDJ_EVD_QALL
 #define SVDJ_EVD_QALL 0
 #endif
+// Split-K slab loads in flight per thread while the EVD assembles G (with
+// many GPUs a pair has up to 64 slabs of its Gram to sum, 1 MB for one
+// workgroup).  8, 16 and 32 measured the same (8-GPU rank plan 59.5 / 60.0 /
+// 59.9 ms per sweep, tools/gpu_r2_slab.sh): the slab sum is not what the
+// EVD's latency is made of.
+#ifndef SVDJ_EVD_SLAB_UNROLL
+#define SVDJ_EVD_SLAB_UNROLL 8
+#endif
 #ifndef SVDJ_EVD_THREADS_32
 #define SVDJ_EVD_THREADS_32 1024
 #endif
@@ -844,7 +852,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         double acc[EV];
 #pragma unroll
         for (int u = 0; u < EV; ++u) acc[u] = 0.0;
-#pragma unroll 8
+#pragma unroll SVDJ_EVD_SLAB_UNROLL
         for (int k = 0; k < nchunk; ++k) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)k * 4 * W * W + gi * EV);
           const T* e = reinterpret_cast<const T*>(&v);
@@ -868,7 +876,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         double acc[EV];
 #pragma unroll
         for (int u = 0; u < EV; ++u) acc[u] = 0.0;
-#pragma unroll 8
+#pragma unroll SVDJ_EVD_SLAB_UNROLL
         for (int k = 0; k < nchunk; ++k) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)k * W * W + gi * EV);
           const T* e = reinterpret_cast<const T*>(&v);
