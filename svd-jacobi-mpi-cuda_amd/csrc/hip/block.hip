@@ -1463,7 +1463,8 @@ __global__ __launch_bounds__(1024) void evd_bip_reg_kernel(
 #ifndef SVDJ_APPLY_QFRAG
 #define SVDJ_APPLY_QFRAG 2
 #endif
-// Row-layout Q fill: 0 element-wise (default), 1 16-byte copies.  The
+// Row-layout Q fill: 0 element-wise (default), 1 16-byte copies, 2 LDS-DMA
+// (global_load_lds, fp32).  The
 // 16-byte fill measured slower: 16384^2 rank plans P=2/4/8 206.5/125.5/62.7
 // -> 215.1/130.9/64.9 ms per sweep, 1 GPU 5.75 -> 5.79 s (tools/gpu_r2_q16*.sh)
 #ifndef SVDJ_APPLY_Q16
@@ -1556,7 +1557,20 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
         Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = q[u];
       }
     }
-  } else if constexpr (SVDJ_APPLY_Q16) {
+  } else if constexpr (SVDJ_APPLY_Q16 == 2 && sizeof(T) == 4 && LDQ == N) {
+    // LDS-DMA fill (global_load_lds_dwordx4): no VGPRs, no ds_write; the
+    // image is the same row-major Q (lane-linear 16-byte pieces)
+    constexpr int PIECES = N * N * (int)sizeof(T) / (NTH * 16);
+    static_assert(PIECES * NTH * 16 == N * N * (int)sizeof(T), "whole pieces");
+    const char* src = reinterpret_cast<const char*>(Qg);
+    char* dst = reinterpret_cast<char*>(Qs);
+#pragma unroll
+    for (int it = 0; it < PIECES; ++it) {
+      const int wb = (it * NTH + wave * 64) * 16;
+      __builtin_amdgcn_global_load_lds(src + wb + lane * 16, dst + wb, 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if constexpr (SVDJ_APPLY_Q16 == 1) {
     for (int iv = threadIdx.x; iv < N * N / VEC; iv += NTH) {
       const int i = iv * VEC;  // VEC consecutive columns of one row (N % VEC == 0)
       *reinterpret_cast<QV*>(&Qs[(i / N) * LDQ + (i % N)]) = Qgv[iv];
