@@ -1458,6 +1458,12 @@ __global__ __launch_bounds__(1024) void evd_bip_reg_kernel(
 #ifndef SVDJ_APPLY_EARLY
 #define SVDJ_APPLY_EARLY 0
 #endif
+// X tiles in flight per wave: 1 (the next tile during this tile's MFMAs) or 2
+// (LDS already caps the apply at two waves per SIMD, so the third tile's 64
+// VGPRs cost no occupancy)
+#ifndef SVDJ_APPLY_DEPTH
+#define SVDJ_APPLY_DEPTH 1
+#endif
 // Q in A-operand fragment order: 0 never, 1 always, 2 for fp64 only (default:
 // fp64 W=64 apply 912 -> 845 us, fp32 W=64 319 -> 338 us, tools/gpu_r2_qfrag.sh)
 #ifndef SVDJ_APPLY_QFRAG
@@ -1583,11 +1589,19 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
 #if !SVDJ_APPLY_EARLY
   load_tile(xv, r0);
 #endif
+#if SVDJ_APPLY_DEPTH >= 2
+  T x1[NK];  // the tile after this one; xn below is two ahead
+  if (r0 + WAVES * TL < r_end) load_tile(x1, r0 + WAVES * TL);
+#endif
   while (true) {
     const int rn = r0 + WAVES * TL;
     const bool more = rn < r_end;
     T xn[NK];
+#if SVDJ_APPLY_DEPTH >= 2
+    if (rn + WAVES * TL < r_end) load_tile(xn, rn + WAVES * TL);
+#else
     if (more) load_tile(xn, rn);  // next tile in flight during this tile's MFMAs
+#endif
     if constexpr (!kHoistQ) asm volatile("" ::: "memory");
     constexpr int kCtUnroll = kHoistQ ? NCT : 1;
 #pragma unroll kCtUnroll
@@ -1630,7 +1644,14 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     }
     if (!more) break;
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk) xv[kk] = xn[kk];
+    for (int kk = 0; kk < NK; ++kk) {
+#if SVDJ_APPLY_DEPTH >= 2
+      xv[kk] = x1[kk];
+      x1[kk] = xn[kk];
+#else
+      xv[kk] = xn[kk];
+#endif
+    }
     r0 = rn;
   }
 }
