@@ -398,8 +398,10 @@ def main():
     p.add_argument("--chains", type=int, default=2)
     p.add_argument("--inner-order", default=svdj_default_inner(), choices=["cyclic", "bipartite"],
                    help="EVD ordering of the block cross steps")
-    p.add_argument("--no-stagger", action="store_true",
-                   help="issue the two step chains independently (lockstep) instead of offset")
+    p.add_argument("--stagger", dest="stagger", action="store_true", default=None,
+                   help="offset the two step chains by an EVD (svdj_block_steps2)")
+    p.add_argument("--no-stagger", dest="stagger", action="store_false",
+                   help="issue the two step chains independently (the default)")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
                    help="block apply matrix cores (auto = native f32/f64 MFMA; bf16x6/bf16x3 "
                         "split modes are faster but not fp32-accurate on every input)")
@@ -430,7 +432,7 @@ def main():
     work = torch.float64 if dtype == torch.float64 else torch.float32
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps, tol=a.tol,
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
-                            stagger=not a.no_stagger, precondition=a.precondition,
+                            stagger=bool(a.stagger), precondition=a.precondition,
                             inner_order=a.inner_order,
                             progress=a.progress, comm_timing=a.gpus > 1)
     if not torch.cuda.is_available():
@@ -522,7 +524,7 @@ def main():
                 "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
                 "inner_order": a.inner_order,
-                "staggered": not a.no_stagger,
+                "staggered": bool(a.stagger),
                 "root_owned": a.root_owned,
             },
             "sweeps": sweeps,
