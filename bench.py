@@ -361,7 +361,8 @@ def run_native(a, dtype, work):
                        "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
                        "mma": "native", "precondition": "none", "chains": 2,
-                       "inner_order": a.inner_order, "staggered": True, "root_owned": False},
+                       "inner_order": a.inner_order,
+                       "staggered": os.environ.get("SVDJ_DIST_STAGGER") == "1", "root_owned": False},
             "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
             "accuracy": acc,

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
@@ -275,6 +276,18 @@ extern "C" int svdj_dist_plan(int world, int rank, int32_t* out, int cap) {
   return (int)groups.size();
 }
 
+// Two chains of a group: issued independently (default) or offset by an EVD
+// (svdj_block_steps2, SVDJ_DIST_STAGGER=1) -- the Python executor's
+// SolverConfig.stagger; independent issue measured faster since the
+// bipartite EVD and the round-2 apply geometry (profiles/r2_stag2).
+static bool stagger_on() {
+  static const bool on = [] {
+    const char* e = getenv("SVDJ_DIST_STAGGER");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   const int P = p->world, g = p->rank, W = p->W, B = p->B;
   const int k = B / W, hk = k / 2, hB = hk * W;
@@ -419,7 +432,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         }
       }
       const Task &x = *t[0]->task;
-      if (n_t == 2) {
+      if (n_t == 2 && stagger_on()) {
         const Task& y = *t[1]->task;
         const int cx = t[0]->stream, cy = t[1]->stream;
         SVDJC(svdj_block_steps2(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
@@ -427,10 +440,13 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
                                 y.pairs, y.npairs, y.steps, y.modes.data(), ws[cy], wsb, st[cy],
                                 p->tol, p->tol_mode, 1, metric, p->mma));
       } else {
-        const int cx = t[0]->stream;
-        SVDJC(svdj_block_steps(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
-                               x.pairs, x.npairs, x.steps, x.modes.data(), p->tol, p->tol_mode, 1,
-                               ws[cx], wsb, metric, p->mma, st[cx]));
+        for (int q = 0; q < n_t; ++q) {  // one chain, or two issued independently
+          const Task& z = *t[q]->task;
+          const int cz = t[q]->stream;
+          SVDJC(svdj_block_steps(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
+                                 z.pairs, z.npairs, z.steps, z.modes.data(), p->tol, p->tol_mode, 1,
+                                 ws[cz], wsb, metric, p->mma, st[cz]));
+        }
       }
       for (int q = 0; q < n_t; ++q) {
         hipEvent_t e = ev[q == 0 ? gr.a : gr.b];
