@@ -142,7 +142,10 @@ DIST_DRIVER_BIN = PKG / "bin" / "svdj_dist_main"
 
 def build_dist(force: bool = False, verbose: bool = False) -> Path:
     """Native distributed solver (svdj_dist.h: RCCL tournament over the HIP
-    block kernels) and its fork launcher ``bin/svdj_dist_main``."""
+    block kernels) and its fork launcher ``bin/svdj_dist_main``.
+
+    Returns the shared library ``DIST_LIB`` (the thing ``ctypes`` loads); the
+    launcher is at ``DIST_DRIVER_BIN``."""
     cpu, hip = build_cpu(force, verbose), build_hip(force, verbose)
     deps = [DIST_SRC, cpu, hip, Path(__file__)] + HEADERS
     if force or _stale(DIST_LIB, deps):
@@ -158,13 +161,13 @@ def build_dist(force: bool = False, verbose: bool = False) -> Path:
               f"-I{CSRC / 'include'}", DIST_DRIVER_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_dist",
               "-lsvdj_hip", "-lsvdj_cpu", "-lrccl", "-Wl,-rpath,$ORIGIN/../lib"], verbose)
         os.replace(tmp, DIST_DRIVER_BIN)
-    return DIST_DRIVER_BIN
+    return DIST_LIB
 
 
 def build_all(force: bool = False, verbose: bool = False) -> dict:
     return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose)),
             "driver": str(build_driver(force, verbose)),
-            "dist": str(build_dist(force, verbose))}
+            "dist": str(build_dist(force, verbose)), "dist_driver": str(DIST_DRIVER_BIN)}
 
 
 if __name__ == "__main__":

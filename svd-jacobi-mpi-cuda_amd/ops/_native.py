@@ -151,6 +151,16 @@ class DistProblem(C.Structure):
                 ("converged", c_int)]
 
 
+def dist_lib_path() -> Path:
+    """Path of libsvdj_dist.so, (re)built unless SVDJ_NO_AUTOBUILD=1.  Always
+    the shared object, never the ``bin/svdj_dist_main`` launcher."""
+    from .. import _build
+
+    if os.environ.get("SVDJ_NO_AUTOBUILD") != "1":
+        _build.build_dist()
+    return _build.DIST_LIB
+
+
 def dist_lib():
     """Native distributed solver (libsvdj_dist.so: RCCL tournament over the
     HIP block kernels, no Python in the sweep).  Loaded after torch, so its
@@ -162,11 +172,7 @@ def dist_lib():
     with _lock:
         if _dist is not None:
             return _dist
-        from .. import _build
-
-        path = _build.DIST_LIB
-        if os.environ.get("SVDJ_NO_AUTOBUILD") != "1":
-            path = _build.build_dist()
+        path = dist_lib_path()
         if not path.exists():
             raise NativeError(f"{path} missing")
         lib = C.CDLL(str(path))

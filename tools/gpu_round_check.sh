@@ -1,7 +1,7 @@
 # GPU check used during development: gpu tests, default bench, kernel profile.
 # Usage (from the repo root, via gpurun):  bash tools/gpu_round_check.sh [N]
 set -o pipefail
-export SVDJ_NO_AUTOBUILD=1
+# Same environment as the driver: no SVDJ_* overrides (autobuild on; in-tree libs are current).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=${1:-16384}
 mkdir -p gpurun_out
