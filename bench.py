@@ -396,7 +396,7 @@ def main():
     p.add_argument("--inner", type=int, default=1)
     p.add_argument("--tol", type=float, default=None,
                    help="rotation threshold (default sqrt(m) eps of the problem dtype)")
-    p.add_argument("--chains", type=int, default=2)
+    p.add_argument("--chains", type=int, default=2, choices=[1, 2])
     p.add_argument("--inner-order", default=svdj_default_inner(), choices=["cyclic", "bipartite"],
                    help="EVD ordering of the block cross steps")
     p.add_argument("--stagger", dest="stagger", action="store_true", default=None,

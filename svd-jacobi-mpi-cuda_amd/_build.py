@@ -103,18 +103,6 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 4) -> Path
     return HIP_LIB
 
 
-def build_hip_variant(name: str, defines: list, verbose: bool = False) -> Path:
-    """Build an A/B variant of the HIP library (extra -D flags) under lib/variants/."""
-    hipcc = _hipcc()
-    out_dir = LIBDIR / "variants"
-    out_dir.mkdir(parents=True, exist_ok=True)
-    out = out_dir / f"libsvdj_hip_{name}.so"
-    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-shared",
-             f"-I{CSRC / 'include'}", f"-I{CSRC / 'hip'}", *[f"-D{d}" for d in defines]]
-    _run([hipcc, *flags, *HIP_SOURCES, "-o", out], verbose)
-    return out
-
-
 DRIVER_SRC = CSRC / "driver" / "svdj_main.cpp"
 DRIVER_BIN = PKG / "bin" / "svdj_main"
 

@@ -73,6 +73,13 @@ class SolverConfig:
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
 
+    def __post_init__(self):
+        if self.chains not in (1, 2):
+            raise ValueError(f"chains must be 1 (blocking exchange) or 2 (pipelined), "
+                             f"got {self.chains}")
+        if self.max_inner_sweeps < 0 or self.max_sweeps < 0:
+            raise ValueError("max_sweeps / max_inner_sweeps must be >= 0")
+
     def bf16_mode(self, A: torch.Tensor | None = None) -> bool:
         """bf16 problem: bf16 in/out, fp32 master copies of A and V, block
         apply on bf16 matrix cores (2-way split) and a bf16-level stop test."""

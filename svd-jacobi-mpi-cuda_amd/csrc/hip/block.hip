@@ -52,12 +52,10 @@ enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2 };
 template <typename T, int W>
 __host__ __device__ constexpr int gram_xsplit() { return (sizeof(T) == 8 && W == 64) ? 2 : 1; }
 
-// Rows per lane per slab of the fp32 W=64 cross Gram (16 = 64 bytes, the
-// default).  8 or 4 cut registers (208 -> 172) but measured slower end to end
-// (16384^2 1 GPU 5.76 -> 6.08 s, 8-GPU rank plan 63.8 -> 73 ms, gpu_r2_lpl.sh).
-#ifndef SVDJ_GRAM_LPL64
-#define SVDJ_GRAM_LPL64 16
-#endif
+// Rows per lane per slab of the fp32 W=64 cross Gram (16 = 64 bytes).  8 or
+// 4 cut registers (208 -> 172) but measured slower end to end (16384^2 1 GPU
+// 5.76 -> 6.08 s, 8-GPU rank plan 63.8 -> 73 ms; round 2).
+constexpr int kGramLpl64 = 16;
 // NV consecutive elements of one column with 16-byte vector loads.
 template <typename T, int NV>
 __device__ __forceinline__ void load_col16B(const T* __restrict__ p, T (&v)[NV]) {
@@ -85,9 +83,8 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   constexpr int HTX = HT / XS;                           // x tiles of this workgroup
   constexpr int NCT = FULL ? 2 * HT : HTX + HT;          // column tiles loaded
   constexpr int NTP = FULL ? NCT * (NCT + 1) / 2 : HTX * HT;
-  // rows per lane per slab: 64 bytes (SVDJ_GRAM_LPL64 for the fp32 W=64
-  // cross Gram)
-  constexpr int LPL = (sizeof(T) == 4 && W == 64 && !FULL) ? SVDJ_GRAM_LPL64 : M::LPL;
+  // rows per lane per slab: 64 bytes
+  constexpr int LPL = (sizeof(T) == 4 && W == 64 && !FULL) ? kGramLpl64 : M::LPL;
   constexpr int SR = M::KG * LPL;  // rows per wave per slab
   constexpr int SLAB = FULL ? 4 * W * W : HTX * TL * W;  // this workgroup's reduction
   constexpr int WAVES = kGramThreads / SVDJ_WAVE;
@@ -229,124 +226,6 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   }
 }
 
-// ------------------------------------------------- gram, LDS-staged (fp32)
-// Cross Gram C = A_bi^T A_bj for fp32 W = 64 with the rows streamed through
-// LDS by LDS-DMA (global_load_lds_dwordx4), the form the CDNA4 playbook gives
-// for an MFMA operand that is read once: the register-fragment loads of
-// gram_kernel touch 32 columns x 16 bytes per instruction (32 partial cache
-// lines) and keep one 16 KB slab per wave in flight; they reached ~2.4-2.9
-// TB/s (profiles/r1_s4_pmc).  Here every wave instruction fetches 8 whole
-// 128-byte column segments, a 4-deep ring keeps 3 stages (48 KB) per
-// workgroup in flight without spending VGPRs, and each wave owns one 32 x 32
-// output tile, written straight to its slab (no cross-wave reduction).
-//
-// Stage = 32 rows x 128 columns (block bi's 64, then bj's 64) = 16 KB, one
-// 128-byte line per column.  Chunk q (rows 4q..4q+3) of column c sits at
-// 16-byte slot q ^ ((c >> 1) & 7) of the column's line: the fragment reads
-// (ds_read_b128, lanes = 16 columns per LDS cycle group) are then
-// conflict-free, and the DMA keeps its lane-linear LDS destination because
-// the swizzle is applied to the per-lane GLOBAL address.  MFMA u = 4v + e of
-// a stage takes row 8v + e (k = 0 lanes) and 8v + 4 + e (k = 1): each lane
-// reads chunk 2v + k of its column once per 4 MFMAs.
-//
-// Ordering (one barrier per stage): wait for this wave's DMAs of stage it
-// (counted vmcnt: the 2 later stages stay in flight) -> s_barrier (every
-// wave's stage-it DMAs retired; every wave's reads of stage it-1 retired by
-// its lgkmcnt(0)) -> DMA stage it+3 into stage it-1's buffer -> read + MFMA.
-// Raw s_barrier, not __syncthreads(): the latter's fence would drain the
-// in-flight DMAs (vmcnt(0)).  All LDS of the kernel is this one array.
-constexpr int kGramLdsKT = 32;  // rows per stage
-
-__device__ __forceinline__ void gram_lds_wait(int ahead) {
-  // this wave issued 4 DMAs per stage; `ahead` later stages may stay in flight
-  if (ahead >= 2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (ahead == 1)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int NS>  // ring depth: NS - 1 stages in flight (2..4)
-__global__ __launch_bounds__(kGramThreads) void gram_lds_kernel(
-    const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
-    int rows_per_chunk, float* __restrict__ slabs) {
-  static_assert(NS >= 2 && NS <= 4, "gram ring depth");
-  constexpr int W = 64, KT = kGramLdsKT;
-  constexpr int STAGE = 2 * W * KT;  // floats per stage
-  __shared__ __attribute__((aligned(16))) float lds[NS * STAGE];
-
-  const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
-  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r_begin = chunk * rows_per_chunk;
-  const int r_end = min(m_pad, r_begin + rows_per_chunk);
-  const int nst = (r_end - r_begin) / KT;
-
-  // DMA source of this lane: instruction d (0..3) of this wave covers stage
-  // columns 32 * wave + 8 d .. +7; lane -> column + 8 * (lane >> 3), slot lane & 7
-  const float* src[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int c = 32 * wave + 8 * d + (lane >> 3);
-    const int q = (lane & 7) ^ ((c >> 1) & 7);
-    const int col = (c < W ? bi : bj) * W + (c & (W - 1));
-    src[d] = A + (size_t)col * lda + r_begin + 4 * q;
-  }
-  auto issue = [&](int s) {  // stage s -> buffer s % NS
-    float* dst = lds + (s % NS) * STAGE + (32 * wave) * KT;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-      __builtin_amdgcn_global_load_lds(src[d] + (size_t)s * KT, dst + 8 * d * KT, 16, 0, 0);
-  };
-
-  // this wave's output tile: X columns 32 a.., Y columns 32 b..
-  const int a = wave >> 1, b = wave & 1;
-  const int i = lane & 31, k = lane >> 5;
-  const int cx = 32 * a + i, cy = W + 32 * b + i;
-  int offx[4], offy[4];  // float offsets of chunk 2v + k inside a stage
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int q = 2 * v + k;
-    offx[v] = cx * KT + 4 * (q ^ ((cx >> 1) & 7));
-    offy[v] = cy * KT + 4 * (q ^ ((cy >> 1) & 7));
-  }
-
-  f32x16 acc;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-
-  for (int s = 0; s < NS - 1 && s < nst; ++s) issue(s);
-  for (int it = 0; it < nst; ++it) {
-    const int ahead = min(nst - 1 - it, NS - 2);
-    gram_lds_wait(ahead);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (it + NS - 1 < nst) issue(it + NS - 1);
-    const float* st = lds + (it % NS) * STAGE;
-    f32x4 xv[4], yv[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      xv[v] = *reinterpret_cast<const f32x4*>(st + offx[v]);
-      yv[v] = *reinterpret_cast<const f32x4*>(st + offy[v]);
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[v][e], yv[v][e], acc, 0, 0, 0);
-    // this wave's reads of the stage are retired before the next barrier
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-
-  float* out = slabs + ((size_t)pair * nchunk + chunk) * (W * W);
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int r = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * k;
-    out[r * W + 32 * b + i] = acc[e];
-  }
-}
-
 // -------------------------------------------------------------------- evd
 // The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair, as a
 // cyclic parallel Jacobi (circle-method round robin: W disjoint rotations per
@@ -376,26 +255,12 @@ struct alignas(2 * sizeof(T)) Pair2 {
   T x, y;
 };
 
-#ifndef SVDJ_EVD_QALL
-#define SVDJ_EVD_QALL 0
-#endif
 // Split-K slab loads in flight per thread while the EVD assembles G (with
 // many GPUs a pair has up to 64 slabs of its Gram to sum, 1 MB for one
 // workgroup).  8, 16 and 32 measured the same (8-GPU rank plan 59.5 / 60.0 /
-// 59.9 ms per sweep, tools/gpu_r2_slab.sh): the slab sum is not what the
-// EVD's latency is made of.
-#ifndef SVDJ_EVD_SLAB_UNROLL
+// 59.9 ms per sweep): the slab sum is not what the EVD's latency is made of.
 #define SVDJ_EVD_SLAB_UNROLL 8
-#endif
-#ifndef SVDJ_EVD_THREADS_32
-#define SVDJ_EVD_THREADS_32 1024
-#endif
-#ifndef SVDJ_EVD_THREADS_64
-#define SVDJ_EVD_THREADS_64 1024
-#endif
-__host__ __device__ constexpr int evd_threads(int W) {
-  return W == 64 ? SVDJ_EVD_THREADS_64 : SVDJ_EVD_THREADS_32;
-}
+__host__ __device__ constexpr int evd_threads(int) { return 1024; }
 
 // Lane i <- lane i-1 / i+1 across the wave (DPP wave_shr:1 / wave_shl:1).
 // The edge lane receives 0 (bound_ctrl); every caller overwrites the edge
@@ -479,17 +344,6 @@ __device__ __forceinline__ double rsqrt64(double x) {
   y = y * (1.5 - hx * y * y);
   return y;
 }
-
-#ifdef SVDJ_EVD_PROFILE
-// Development instrumentation: per-phase cycle totals of one EVD workgroup
-// (pair 0), read back with svdj_debug_evd_profile().
-__device__ unsigned long long g_evd_prof[16];
-#define EVD_T(i) unsigned long long _t##i = (pair == 0 && (tid == 0 || tid == NT - 64)) ? clock64() : 0
-#define EVD_ACC(k, a, b) if (pair == 0 && (tid == 0 || tid == NT - 64)) atomicAdd(&g_evd_prof[(tid == 0 ? 0 : 8) + k], _t##b - _t##a)
-#else
-#define EVD_T(i)
-#define EVD_ACC(k, a, b)
-#endif
 
 // Circle-method players of slot a at step st (the same movement as the DPP
 // shifts of the register Q: firsts move right, seconds left, player N-1 fixed
@@ -695,9 +549,6 @@ __host__ __device__ constexpr int block_duty_o(int a, int b) {  // 256*e + meeti
 // instead -- the same duty blocks, the other blocks placed so the 32 lanes of
 // each LDS lane group hit distinct banks where possible (modelled LDS cycles
 // per step W=64: 1144 -> 812, conflict share 45 -> 22 %).
-#ifndef SVDJ_EVD_DEAL_OPT
-#define SVDJ_EVD_DEAL_OPT 1
-#endif
 template <int W, int NT, int ORD = EVD_CYCLIC, bool OPT = false>
 struct EvdDeal {
   static constexpr int NOFF = W * (W - 1) / 2;
@@ -759,7 +610,7 @@ static_assert(evd_deal_ok<32, 1024, EVD_BIP, true>(), "optimised EVD block deali
 // which dealing a kernel uses
 template <typename T, int W, int NT, int ORD>
 __host__ __device__ constexpr bool evd_deal_opt() {
-  return SVDJ_EVD_DEAL_OPT && sizeof(T) == 4 && ORD == EVD_BIP && NT == 1024 && (W == 32 || W == 64);
+  return sizeof(T) == 4 && ORD == EVD_BIP && NT == 1024 && (W == 32 || W == 64);
 }
 
 template <typename T, int W, int ORD>
@@ -774,23 +625,16 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   constexpr int R = O::R;               // steps per sweep
   constexpr int NTRI = N * (N - 1) / 2;
   constexpr int GPW = SVDJ_WAVE / W;    // Q row groups per wave
-  // Q row groups: waves 1..NWAVE-1, or every wave (SVDJ_EVD_QALL).  Since
-  // the step loop is unrolled the solver wave is no longer the slowest
-  // (16384^2 8-GPU shape, W=64: wave 0 1357 cycles per step, a Q wave ~1440
-  // of G update + ~300 of Q), but giving it Q rows measured neutral
-  // (profiles/r2_evd_unroll): the step is bound by the G update's LDS
-  // traffic, not by the Q rows.
-  constexpr int QW0 = SVDJ_EVD_QALL ? 0 : 1;  // first Q wave
+  // Q row groups: waves 1..NWAVE-1 (wave 0 solves).  Giving the solver wave
+  // Q rows as well measured neutral (round 2, profiles/r2_evd_unroll): the
+  // step is bound by the G update's LDS traffic, not by the Q rows.
+  constexpr int QW0 = 1;  // first Q wave
   constexpr int NGRP = (NWAVE - QW0) * GPW;
   constexpr int RPL = (N + NGRP - 1) / NGRP;  // Q rows per lane (the last group may idle)
   constexpr bool DOPT = evd_deal_opt<T, W, NT, ORD>();
   constexpr int MAXOFF = EvdDeal<W, NT, ORD, DOPT>::MAXOFF;
   static_assert(W >= 4 && W <= 64 && NWAVE >= 2, "EVD geometry");
-#ifdef SVDJ_EVD_Q32
-  using QT = T;
-#else
-  using QT = double;
-#endif
+  using QT = double;  // fp32 Q measured 8 % faster with 10x worse V orthogonality
   static constexpr EvdDeal<W, NT, ORD, DOPT> deal{};
 
   __shared__ T Gb[2][NTRI + 1];  // off-diagonal G by position pair, double-buffered;
@@ -813,7 +657,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  EVD_T(9);
 
   // ---- assemble G: diagonal first (player order), then every off-diagonal
   // entry into position space for step 0; split-K slabs summed in fp64
@@ -989,8 +832,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     pend = rot ? T(0) : gpq;
     publish(0, tid, c, s, t, gpp - t * gpq, gqq + t * gpq);
   }
-  EVD_T(8);
-  EVD_ACC(4, 9, 8);
   __syncthreads();
 
   // One block's update J^T G J (entries moved to their next-step positions)
@@ -1068,9 +909,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   // loop-invariant register plus an immediate.  Returns true when done.
   auto step = [&](auto parity) -> bool {
     constexpr int b = decltype(parity)::value, nb = b ^ 1;
-    EVD_T(0);
     const bool last = st + 1 == R;  // this phase solves step 0 of the next sweep
-    if (wave == 0 && !SVDJ_EVD_QALL) {
+    if (wave == 0) {
       // solver wave: its duty blocks (lanes < W, j = 0) and nothing else of Q
       update_blocks(b, nb, true, last);
       if (last) {  // every rotation of sweep sw is decided by now
@@ -1079,40 +919,11 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
         racc = racc_next;
         racc_next = 0;
       }
-      EVD_T(1);
-      EVD_T(2);
-      EVD_ACC(1, 1, 2);
-      EVD_ACC(0, 0, 1);
-    } else if (wave == 0) {
-      // solver wave with Q rows: duty blocks, then its Q share
-      const QT2 rqs = rq[b][slot];
-      const QT cq = rqs.x, sq = rqs.y;
-      update_blocks(b, nb, true, last);
-      if (last) {
-        const int rot = __any(racc) ? 1 : 0;
-        if (lane == 0) rot_flag[sw & 1] = rot;
-        racc = racc_next;
-        racc_next = 0;
-      }
-      EVD_T(1);
-#pragma unroll
-      for (int i = 0; i < RPL; ++i) {
-        const QT x = qf[i], y = qs[i];
-        qf[i] = cq * x - sq * y;
-        qs[i] = sq * x + cq * y;
-      }
-#pragma unroll
-      for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
-      O::move(pf, ps, slot);
-      EVD_T(2);
-      EVD_ACC(1, 1, 2);
-      EVD_ACC(0, 0, 1);
     } else {
       // Q waves: this step's Q rotation (records read up front)
       const QT2 rqs = rq[b][slot];
       const QT cq = rqs.x, sq = rqs.y;
       update_blocks(b, nb, false, last);
-      EVD_T(1);
       // Q <- Q J in registers (c = 1, s = 0 for no rotation)
 #pragma unroll
       for (int i = 0; i < RPL; ++i) {
@@ -1124,13 +935,8 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 #pragma unroll
       for (int i = 0; i < RPL; ++i) O::move(qf[i], qs[i], slot);
       O::move(pf, ps, slot);
-      EVD_T(2);
-      EVD_ACC(0, 0, 1);
-      EVD_ACC(1, 1, 2);
     }
     __syncthreads();
-    EVD_T(3);
-    EVD_ACC(2, 0, 3);
     ++gs;
     if (++st < R) return false;
     st = 0;
@@ -1141,8 +947,6 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   if (run && max_inner > 0)
     while (!step(std::integral_constant<int, 0>{}) && !step(std::integral_constant<int, 1>{})) {
     }
-  EVD_T(7);
-  EVD_ACC(5, 8, 7);
 
   if (tid == 0) {
     skip[pair] = any ? 0 : 1;
@@ -1175,312 +979,11 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
 }
 
-// ------------------------------------------- evd, register-resident (bip)
-// The bipartite cross-step EVD (fp32 W = 64) with G held in REGISTERS in slot
-// space instead of LDS in position space.  The LDS kernel above is bound by
-// its G update: ~25 LDS instructions per thread and step at a 38 % bank
-// conflict share (profiles/r2_evd_unroll), and the EVD is the part of a step
-// the other chain cannot hide once a GPU holds few pairs
-// (tools/trace_crit.py: EVD-only time 2.6 % of a 1-GPU sweep, 24 % at 8 GPUs).
-//
-// Slot space: 2 x 2 blocks B(i, j) = [[G(X_i, X_j), G(X_i, Y_j)],
-// [G(Y_i, X_j), G(Y_i, Y_j)]], X_i column i of block bi (fixed), Y_j the
-// column of block bj at slot j in the current step (slot j pairs X_j with
-// Y_j; every step slot j+1's Y moves to slot j, Ord<W, EVD_BIP>).  The block
-// matrix is held by DIAGONAL: thread (wave w, lane l) holds B(l, l + d) for
-// d = 4w + r, r = 0..3 (16 fp32 registers), so
-//   * wave 0, r = 0 holds every diagonal block B(k, k): wave 0 alone solves
-//     the next step's 64 rotations, from registers (G(X_k, Y_{k+1}) is its
-//     r = 1 entry, G(Y_{k+1}, Y_{k+1}) one DPP lane away), no divergence;
-//   * a block's row rotation is the lane's slot (one record read), its column
-//     rotation slot l + d (four consecutive records);
-//   * the Y move is a register move along d for G(X, Y) (d + 1), a DPP lane
-//     rotate plus a register move for G(Y, X) (i + 1, d - 1) and a DPP lane
-//     rotate for G(Y, Y); the two register moves that cross a wave go through
-//     a 64-entry LDS exchange read after the next barrier.
-// The 2 x 2 updates run as packed fp32 (v_pk_fma_f32 on register pairs).
-// Q as in the LDS kernel's slot layout, fp64, 8 rows per thread on all waves.
-// ONE barrier per step; ~12 LDS instructions per thread and step (against
-// ~25), no bank conflicts.
-//
-// Same rotations, order, stop test, skip rule and outputs (Q, D, skip,
-// metric) as evd_kernel<float, 64, EVD_BIP>: tests/test_gpu_kernels.py checks
-// it against the fp64 reference with the bipartite ordering and against the
-// LDS kernel.
-//
-// Measured (profiles/r2_evdreg): correct, but SLOWER end to end (8-GPU rank
-// plan 66.4 -> 80.3 ms per sweep; a first row-major version that solved in
-// every wave 95.9).  It is VALU-issue bound: holding both triangles doubles
-// the G arithmetic the LDS kernel does on its packed triangle, the fp64 Q
-// rotation costs the same in both, and ~200 VALU instructions per wave and
-// step at four waves per SIMD exceed the LDS kernel's LDS-bound step.  Off by
-// default (SVDJ_EVD_REG=1 turns it on).
-#ifndef SVDJ_EVD_REG_DEFAULT
-#define SVDJ_EVD_REG_DEFAULT 0
-#endif
-using f32x2 = __attribute__((ext_vector_type(2))) float;
-__global__ __launch_bounds__(1024) void evd_bip_reg_kernel(
-    const int32_t* __restrict__ pairs, const float* __restrict__ slabs, int nchunk,
-    float* __restrict__ D, float* __restrict__ Qout, int32_t* __restrict__ skip, float tol,
-    int absmode, int max_inner, uint32_t* __restrict__ metric) {
-  constexpr int W = 64, N = 2 * W, NT = 1024, NWAVE = NT / 64;
-  constexpr int RB = W / NWAVE;   // diagonals per thread (4)
-  constexpr int RQ = N / NWAVE;   // Q rows per thread (8)
-  using f2 = Pair2<float>;
-  using d2 = Pair2<double>;
-  __shared__ float Cs[W][W + 1];   // summed cross Gram
-  __shared__ float dg[N];          // diagonals, players X 0..W-1, Y W..2W-1
-  __shared__ f2 rcs[2][W], rdd[2][W];
-  __shared__ d2 rq[2][W];
-  __shared__ float xxy[2][NWAVE][W];  // every wave's d = 4w entry of G(X, Y) after the update
-  __shared__ float xyx[2][NWAVE][W];  // every wave's d = 4w+3 entry of G(Y, X)
-  __shared__ int rot_flag[2];
-  __shared__ float wmax[NWAVE];
-  __shared__ int wneed[NWAVE];
-  __shared__ int need_any;
-
-  const int pair = blockIdx.x;
-  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  // ---- assemble: diagonals, cross Gram (split-K slabs summed in fp64), the
-  // convergence value and the "anything to rotate" pre-test
-  for (int a = tid; a < N; a += NT) dg[a] = D[a < W ? bi * W + a : bj * W + (a - W)];
-  __syncthreads();
-  {
-    float mx = 0.0f;
-    int need = 0;
-    const float* s0 = slabs + (size_t)pair * nchunk * (W * W);
-    for (int gi = tid; gi < W * W / 4; gi += NT) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-      for (int c = 0; c < nchunk; ++c) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)c * W * W + gi * 4);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] += (double)v[u];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = gi * 4 + u, r = i / W, c = i % W;
-        const float g = (float)acc[u];
-        Cs[r][c] = g;
-        const float grr = dg[r], gcc = dg[W + c];
-        const float d = sqrtf(grr) * sqrtf(gcc);
-        if (d > 0.0f) {
-          const float v = fabsf(g) / d;
-          mx = v > mx ? v : mx;
-        }
-        need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
-      }
-    }
-    mx = wave_max(mx);
-    need = __any(need) ? 1 : 0;
-    if (lane == 0) {
-      wmax[wave] = mx;
-      wneed[wave] = need;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      float m2 = 0.0f;
-      int n2 = 0;
-      for (int w = 0; w < NWAVE; ++w) {
-        m2 = wmax[w] > m2 ? wmax[w] : m2;
-        n2 |= wneed[w];
-      }
-      atomic_max_pos(&metric[0], m2);
-      need_any = n2;
-    }
-    __syncthreads();
-  }
-  const bool run = need_any != 0 && max_inner > 0;
-
-  // ---- registers: B(lane, lane + 4 wave + r) as two packed pairs per entry
-  // kind (r = 0, 1 and r = 2, 3); Q rows 8 wave + u
-  f32x2 xx[2], xy[2], yx[2], yy[2];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const int d = RB * wave + r, j = (lane + d) & (W - 1);
-    xy[r >> 1][r & 1] = Cs[lane][j];
-    yx[r >> 1][r & 1] = Cs[j][lane];
-    xx[r >> 1][r & 1] = d == 0 ? dg[lane] : 0.0f;       // blocks are internally orthogonal
-    yy[r >> 1][r & 1] = d == 0 ? dg[W + lane] : 0.0f;
-  }
-  double qx[RQ], qy[RQ];
-#pragma unroll
-  for (int u = 0; u < RQ; ++u) {
-    const int k = RQ * wave + u;
-    qx[u] = k == lane ? 1.0 : 0.0;
-    qy[u] = k == W + lane ? 1.0 : 0.0;
-  }
-  const bool solver = wave == 0;  // slot k = lane, block B(k, k) in r = 0
-  float my_dp = 0.0f, my_dq = 0.0f, my_g = 0.0f;
-  bool my_rot = false;
-  auto publish = [&](int b, int k, float c, float s, float t, float dp, float dq) {
-    rcs[b][k] = f2{c, s};
-    rdd[b][k] = f2{dp, dq};
-    const double td = (double)t, c64 = rsqrt64(fma(td, td, 1.0));
-    rq[b][k] = d2{c64, td * c64};
-  };
-  int racc = 0, racc_next = 0;
-  if (run && solver) {  // step 0's rotations
-    const float gpp = xx[0][0], gqq = yy[0][0], gpq = xy[0][0];
-    float c, s, t;
-    my_rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
-    racc = my_rot;
-    my_g = gpq;
-    my_dp = gpp - t * gpq;
-    my_dq = gqq + t * gpq;
-    publish(0, lane, c, s, t, my_dp, my_dq);
-  }
-  __syncthreads();
-
-  bool any = false;
-  int gs = 0, sw = 0, st = 0;
-  const int wn = (wave + 1) & (NWAVE - 1), wp = (wave - 1) & (NWAVE - 1);
-  while (run) {
-    const int b = gs & 1, nb = b ^ 1;
-    const bool last = st + 1 == W;  // this phase solves step 0 of the next sweep
-    // deferred wave-crossing moves of the previous step
-    if (gs > 0) {
-      xy[1][1] = xxy[nb][wn][lane];                    // G(X_i, Y_{j+1}), d = 4w + 4
-      yx[0][0] = xyx[nb][wp][(lane + 1) & (W - 1)];    // G(Y_{i+1}, X_j), d = 4w - 1
-    }
-    // this step's rotations: row = slot `lane`, columns = slots lane + d
-    const f2 rr = rcs[b][lane];
-    f2 rcol[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) rcol[r] = rcs[b][(lane + RB * wave + r) & (W - 1)];
-    const d2 rqs = rq[b][lane];
-    // B <- R_i^T B R_j, packed over (r = 0, 1) and (r = 2, 3)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x2 ca = {rr.x, rr.x}, sa = {rr.y, rr.y};
-      const f32x2 cb = {rcol[2 * h].x, rcol[2 * h + 1].x};
-      const f32x2 sb = {rcol[2 * h].y, rcol[2 * h + 1].y};
-      const f32x2 h00 = ca * xx[h] - sa * yx[h], h01 = ca * xy[h] - sa * yy[h];
-      const f32x2 h10 = sa * xx[h] + ca * yx[h], h11 = sa * xy[h] + ca * yy[h];
-      xx[h] = cb * h00 - sb * h01;
-      xy[h] = sb * h00 + cb * h01;
-      yx[h] = cb * h10 - sb * h11;
-      yy[h] = sb * h10 + cb * h11;
-    }
-    if (solver) {  // the rotated pair's own block exactly: diag(d_p', d_q'), coupling 0
-      const float off = my_rot ? 0.0f : my_g;
-      xx[0][0] = my_dp;
-      yy[0][0] = my_dq;
-      xy[0][0] = off;
-      yx[0][0] = off;
-    }
-    xxy[b][wave][lane] = xy[0][0];
-    xyx[b][wave][lane] = yx[1][1];
-    // move to the next step's slots
-    //   G(X_i, Y_j)  <- d + 1           (r + 1; r = 3 from wave w+1 after the barrier)
-    //   G(Y_i, X_j)  <- i + 1, d - 1    (lane + 1, r - 1; r = 0 from wave w-1)
-    //   G(Y_i, Y_j)  <- i + 1           (lane + 1)
-    xy[0][0] = xy[0][1];
-    xy[0][1] = xy[1][0];
-    xy[1][0] = xy[1][1];
-    yx[1][1] = bip_shift<W>(yx[1][0], lane);
-    yx[1][0] = bip_shift<W>(yx[0][1], lane);
-    yx[0][1] = bip_shift<W>(yx[0][0], lane);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      yy[h][0] = bip_shift<W>(yy[h][0], lane);
-      yy[h][1] = bip_shift<W>(yy[h][1], lane);
-    }
-    if (solver) {  // the next step's rotation of slot `lane`
-      const float gpp = xx[0][0], gpq = xy[0][0], gqq = yy[0][0];
-      float c, s, t;
-      my_rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
-      if (last) racc_next |= my_rot; else racc |= my_rot;
-      my_g = gpq;
-      my_dp = gpp - t * gpq;
-      my_dq = gqq + t * gpq;
-      publish(nb, lane, c, s, t, my_dp, my_dq);
-      if (last) {  // every rotation of sweep sw is decided by now
-        const int rot = __any(racc) ? 1 : 0;
-        if (lane == 0) rot_flag[sw & 1] = rot;
-        racc = racc_next;
-        racc_next = 0;
-      }
-    }
-    // Q <- Q J (fp64), then the Y columns move with their players
-#pragma unroll
-    for (int u = 0; u < RQ; ++u) {
-      const double x = qx[u], y = qy[u];
-      qx[u] = rqs.x * x - rqs.y * y;
-      qy[u] = rqs.y * x + rqs.x * y;
-    }
-#pragma unroll
-    for (int u = 0; u < RQ; ++u) qy[u] = bip_shift<W>(qy[u], lane);
-    __syncthreads();
-    ++gs;
-    if (++st < W) continue;
-    st = 0;
-    if (!rot_flag[sw & 1]) break;
-    any = true;
-    if (++sw >= max_inner) break;
-  }
-
-  if (tid == 0) {
-    skip[pair] = any ? 0 : 1;
-    if (any) atomicAdd(&metric[1], 1u);
-  }
-  if (!any) return;  // cross mode: D only changes with a rotation
-  {
-    float* qo = Qout + (size_t)pair * N * N;
-    const int ps = W + ((lane + gs) & (W - 1));  // Y player now at slot `lane`
-#pragma unroll
-    for (int u = 0; u < RQ; ++u) {
-      const int k = RQ * wave + u;
-      qo[k * N + lane] = (float)qx[u];
-      qo[k * N + ps] = (float)qy[u];
-    }
-  }
-  if (tid < W) {  // diagonals after the last executed step (gs - 1)
-    const int lb = (gs - 1) & 1;
-    const int q = W + ((tid + gs - 1) & (W - 1));
-    D[bi * W + tid] = rdd[lb][tid].x;
-    D[bj * W + (q - W)] = rdd[lb][tid].y;
-  }
-}
-
 // ------------------------------------------------------------------ apply
-#ifndef SVDJ_APPLY_QPD
-#define SVDJ_APPLY_QPD 8
-#endif
-#ifndef SVDJ_APPLY_THREADS_64
-#define SVDJ_APPLY_THREADS_64 256
-#endif
-#ifndef SVDJ_APPLY_THREADS_32
-#define SVDJ_APPLY_THREADS_32 256
-#endif
-#ifndef SVDJ_APPLY_EARLY
-#define SVDJ_APPLY_EARLY 0
-#endif
-// X tiles in flight per wave: 1 (the next tile during this tile's MFMAs) or 2
-// (LDS already caps the apply at two waves per SIMD, so the third tile's 64
-// VGPRs cost no occupancy)
-#ifndef SVDJ_APPLY_DEPTH
-#define SVDJ_APPLY_DEPTH 1
-#endif
-// Q in A-operand fragment order: 0 never, 1 always, 2 for fp64 only (default:
-// fp64 W=64 apply 912 -> 845 us, fp32 W=64 319 -> 338 us, tools/gpu_r2_qfrag.sh)
-#ifndef SVDJ_APPLY_QFRAG
-#define SVDJ_APPLY_QFRAG 2
-#endif
-// Row-layout Q fill: 0 element-wise (default), 1 16-byte copies, 2 LDS-DMA
-// (global_load_lds, fp32).  The
-// 16-byte fill measured slower: 16384^2 rank plans P=2/4/8 206.5/125.5/62.7
-// -> 215.1/130.9/64.9 ms per sweep, 1 GPU 5.75 -> 5.79 s (tools/gpu_r2_q16*.sh)
-#ifndef SVDJ_APPLY_Q16
-#define SVDJ_APPLY_Q16 0
-#endif
+// Q fragments are read kQPD k-steps ahead of their MFMA (row-layout Q).
+constexpr int kQPD = 8;
 template <typename T, int W>
-__host__ __device__ constexpr int apply_threads() {
-  return (W == 64 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_64
-                                     : ((W == 32 && sizeof(T) == 4) ? SVDJ_APPLY_THREADS_32 : kApplyThreads);
-}
+__host__ __device__ constexpr int apply_threads() { return kApplyThreads; }
 template <typename T, int W>
 __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     T* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, T* __restrict__ V,
@@ -1539,17 +1042,14 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   };
   int r0 = r_begin + wave * TL;
   T xv[NK];
-#if SVDJ_APPLY_EARLY
-  // the first X tile is independent of Q: its HBM latency overlaps the Q fill
-  if (r0 < r_end) load_tile(xv, r0);
-#endif
   const T* Qg = Qall + (size_t)pair * N * N;
-  // Q in A-operand fragment order (kQFrag): for (column tile, group of VEC
+  // fp64: Q in A-operand fragment order -- for (column tile, group of VEC
   // k-steps, lane) the VEC operands are contiguous, one 16-byte LDS read per
-  // VEC MFMAs
-  constexpr bool kQFrag = SVDJ_APPLY_QFRAG == 1 || (SVDJ_APPLY_QFRAG == 2 && sizeof(T) == 8);
+  // VEC MFMAs (fp64 W=64 apply 912 -> 845 us; fp32 W=64 319 -> 338 us, so
+  // fp32 keeps the row layout with an element-wise fill -- 16-byte and
+  // LDS-DMA fills measured slower or equal, round 2)
+  constexpr bool kQFrag = sizeof(T) == 8;
   constexpr int VEC = 16 / (int)sizeof(T);
-  // 16-byte loads (Q is 16-byte aligned: N*N elements per pair)
   using QV = __attribute__((ext_vector_type(VEC))) T;
   const QV* Qgv = reinterpret_cast<const QV*>(Qg);
   if constexpr (kQFrag) {
@@ -1563,45 +1063,17 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
         Qs[((ct * (NK / VEC) + kk / VEC) * 64 + kgi * TL + lci) * VEC + kk % VEC] = q[u];
       }
     }
-  } else if constexpr (SVDJ_APPLY_Q16 == 2 && sizeof(T) == 4 && LDQ == N) {
-    // LDS-DMA fill (global_load_lds_dwordx4): no VGPRs, no ds_write; the
-    // image is the same row-major Q (lane-linear 16-byte pieces)
-    constexpr int PIECES = N * N * (int)sizeof(T) / (NTH * 16);
-    static_assert(PIECES * NTH * 16 == N * N * (int)sizeof(T), "whole pieces");
-    const char* src = reinterpret_cast<const char*>(Qg);
-    char* dst = reinterpret_cast<char*>(Qs);
-#pragma unroll
-    for (int it = 0; it < PIECES; ++it) {
-      const int wb = (it * NTH + wave * 64) * 16;
-      __builtin_amdgcn_global_load_lds(src + wb + lane * 16, dst + wb, 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if constexpr (SVDJ_APPLY_Q16 == 1) {
-    for (int iv = threadIdx.x; iv < N * N / VEC; iv += NTH) {
-      const int i = iv * VEC;  // VEC consecutive columns of one row (N % VEC == 0)
-      *reinterpret_cast<QV*>(&Qs[(i / N) * LDQ + (i % N)]) = Qgv[iv];
-    }
-  } else {  // element-wise fill (A/B variant)
+  } else {
     for (int i = threadIdx.x; i < N * N; i += NTH) Qs[(i / N) * LDQ + (i % N)] = Qg[i];
   }
   __syncthreads();
   if (r0 >= r_end) return;
-#if !SVDJ_APPLY_EARLY
   load_tile(xv, r0);
-#endif
-#if SVDJ_APPLY_DEPTH >= 2
-  T x1[NK];  // the tile after this one; xn below is two ahead
-  if (r0 + WAVES * TL < r_end) load_tile(x1, r0 + WAVES * TL);
-#endif
   while (true) {
     const int rn = r0 + WAVES * TL;
     const bool more = rn < r_end;
     T xn[NK];
-#if SVDJ_APPLY_DEPTH >= 2
-    if (rn + WAVES * TL < r_end) load_tile(xn, rn + WAVES * TL);
-#else
     if (more) load_tile(xn, rn);  // next tile in flight during this tile's MFMAs
-#endif
     if constexpr (!kHoistQ) asm volatile("" ::: "memory");
     constexpr int kCtUnroll = kHoistQ ? NCT : 1;
 #pragma unroll kCtUnroll
@@ -1620,21 +1092,21 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
           cur = nxt;
         }
       } else {
-      // Q fragments are read SVDJ_APPLY_QPD k-steps ahead of their MFMA
-      // (sched_barrier keeps the order; just in time, each ds_read's latency
-      // sat between two dependent MFMAs).  Two interleaved accumulation
-      // chains per wave were measured slower (1269 vs 1145 us, W=64).
-      constexpr int PD = SVDJ_APPLY_QPD < NK ? SVDJ_APPLY_QPD : NK;
-      T qa[PD];
+        // Q fragments are read kQPD k-steps ahead of their MFMA (sched_barrier
+        // keeps the order; just in time, each ds_read's latency sat between
+        // two dependent MFMAs).  Two interleaved accumulation chains per wave
+        // were measured slower (1269 vs 1145 us, W=64).
+        constexpr int PD = kQPD < NK ? kQPD : NK;
+        T qa[PD];
 #pragma unroll
-      for (int i = 0; i < PD; ++i) qa[i] = Qs[(i * KG + kg) * LDQ + ct * TL + lc];
+        for (int i = 0; i < PD; ++i) qa[i] = Qs[(i * KG + kg) * LDQ + ct * TL + lc];
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const T a = qa[kk % PD];
-        if (kk + PD < NK) qa[kk % PD] = Qs[((kk + PD) * KG + kg) * LDQ + ct * TL + lc];
-        acc = M::mfma(a, xv[kk], acc);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int kk = 0; kk < NK; ++kk) {
+          const T a = qa[kk % PD];
+          if (kk + PD < NK) qa[kk % PD] = Qs[((kk + PD) * KG + kg) * LDQ + ct * TL + lc];
+          acc = M::mfma(a, xv[kk], acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       const int c0 = ct * TL;
       T* dst = (c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld);
@@ -1644,138 +1116,9 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
     }
     if (!more) break;
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk) {
-#if SVDJ_APPLY_DEPTH >= 2
-      xv[kk] = x1[kk];
-      x1[kk] = xn[kk];
-#else
-      xv[kk] = xn[kk];
-#endif
-    }
+    for (int kk = 0; kk < NK; ++kk) xv[kk] = xn[kk];
     r0 = rn;
   }
-}
-
-// ------------------------------------------- apply with X staged in LDS (fp32)
-// Alternative fp32 apply, same math as apply_kernel (Out^T = Q^T X^T, lane =
-// row), with the roles of LDS and registers swapped.  Wave w owns output column
-// tile w: its Q slice (N/2 A-operand values per lane) is loaded once into
-// registers.  The 32-row X tile, which every wave multiplies, is read once
-// per workgroup with 16-byte loads into double-buffered LDS, with one barrier
-// per tile.  The next tile's loads are in flight during this tile's MFMAs.  No
-// per-wave X tile and no prefetch copy in VGPRs, so more waves fit per SIMD
-// than in apply_kernel (selected with SVDJ_APPLY_LDSX=1).
-#ifndef SVDJ_APPLY_XPD
-#define SVDJ_APPLY_XPD 8
-#endif
-#ifndef SVDJ_APPLY_LDSX_WAVES
-#define SVDJ_APPLY_LDSX_WAVES 4
-#endif
-template <int W>
-__global__ __launch_bounds__(4 * W) __attribute__((amdgpu_waves_per_eu(SVDJ_APPLY_LDSX_WAVES)))
-void apply_ldsx_kernel(
-    float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
-    int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
-    const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
-  using M = Mfma<float>;
-  constexpr int N = 2 * W;        // columns of X = [A_bi A_bj]
-  constexpr int NK = N / 2;       // k values per lane (KG = 2)
-  constexpr int NTH = 4 * W;      // N / 32 waves, one per output column tile
-  constexpr int TILE_F = N * 32;  // floats per 32-row X tile, stored [k][row]
-  constexpr int LPT = TILE_F / 4 / NTH;  // 16-byte loads per thread per tile
-  static_assert(LPT == 4 && NTH % 8 == 0, "loader mapping");
-  __shared__ alignas(16) float Xs[2][TILE_F];
-
-  const int pair = blockIdx.x;
-  if (skip[pair]) return;
-  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
-  int chunk = blockIdx.y;
-  float* base;
-  int ld, r_begin, r_end;
-  if (chunk < a_chunks) {
-    base = A;
-    ld = lda;
-    r_begin = chunk * rows_a;
-    r_end = min(m_pad, r_begin + rows_a);
-  } else {
-    chunk -= a_chunks;
-    base = V;
-    ld = ldv;
-    r_begin = chunk * rows_v;
-    r_end = min(n_v, r_begin + rows_v);
-  }
-  if (r_begin >= r_end) return;
-  const int t = threadIdx.x, lane = t & 63, ct = t >> 6;
-  const int lc = M::lane_col(lane), kg = M::lane_kg(lane);
-  float* const xi = base + (size_t)bi * W * ld;
-  float* const xj = base + (size_t)bj * W * ld;
-
-  // loader: 16-byte chunk i*NTH + t of the tile is column k_i = i*NTH/8 + t/8,
-  // rows 4*(t%8) .. +3; k_i < W exactly for i < 2 (t/8 < W/2)
-  const int lrow = 4 * (t & 7);
-  uint32_t goff[LPT];
-  int soff[LPT];
-#pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int k = i * (NTH / 8) + (t >> 3);
-    goff[i] = (uint32_t)((k < W ? k : k - W) * ld + lrow);
-    soff[i] = k * 32 + lrow;
-  }
-  float4 lr[LPT];
-  auto gload = [&](int r0) {
-#pragma unroll
-    for (int i = 0; i < LPT; ++i)
-      lr[i] = *reinterpret_cast<const float4*>((i < 2 ? xi : xj) + goff[i] + (uint32_t)r0);
-  };
-  auto lstore = [&](int b) {
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) *reinterpret_cast<float4*>(&Xs[b][soff[i]]) = lr[i];
-  };
-  gload(r_begin);
-
-  // Q slice of column tile ct: q[kk] = Q[2kk + kg][32 ct + lc]
-  const float* Qg = Qall + (size_t)pair * N * N + kg * N + ct * 32 + lc;
-  float q[NK];
-#pragma unroll
-  for (int kk = 0; kk < NK; ++kk) q[kk] = Qg[(size_t)kk * 2 * N];
-
-  const int c0 = ct * 32;
-  float* const dst = c0 < W ? xi + (size_t)c0 * ld : xj + (size_t)(c0 - W) * ld;
-  const uint32_t st_off = (uint32_t)(M::acc_row_lane(lane) * ld + lc);
-  lstore(0);
-  __syncthreads();
-  constexpr int PD = SVDJ_APPLY_XPD < NK ? SVDJ_APPLY_XPD : NK;
-  for (int it = 0, r0 = r_begin;; ++it, r0 += 32) {
-    const bool more = r0 + 32 < r_end;  // uniform over the workgroup
-    if (more) gload(r0 + 32);
-    // B operand of lane (kg, lc) at step kk: X[row lc][k = 2kk + kg]
-    const float* xs = &Xs[it & 1][kg * 32 + lc];
-    float xa[PD];
-#pragma unroll
-    for (int i = 0; i < PD; ++i) xa[i] = xs[i * 64];
-    typename M::acc_t acc = M::zero();
-#pragma unroll
-    for (int kk = 0; kk < NK; ++kk) {
-      const float b = xa[kk % PD];
-      if (kk + PD < NK) xa[kk % PD] = xs[(kk + PD) * 64];
-      acc = M::mfma(q[kk], b, acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int e = 0; e < M::NACC; ++e)
-      dst[(size_t)M::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = acc[e];
-    if (!more) break;
-    lstore((it + 1) & 1);  // that buffer's last readers passed the previous barrier
-    __syncthreads();
-  }
-}
-
-static bool apply_ldsx_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SVDJ_APPLY_LDSX");
-    return e && atoi(e) != 0;
-  }();
-  return on;
 }
 
 // -------------------------------------------------- apply on bf16 matrix cores
@@ -1790,26 +1133,14 @@ static bool apply_ldsx_enabled() {
 // the X tile is split in registers right after its loads land.
 // Same transposed formulation as apply_kernel: Out^T = Q^T X^T, lane = row.
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
-#ifndef SVDJ_SPLIT_INT
-#define SVDJ_SPLIT_INT 0
-#endif
 
 template <int NP>
 __device__ __forceinline__ void split_bf16(float x, __bf16 (&p)[NP]) {
   float r = x;
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-#if SVDJ_SPLIT_INT
-    // explicit round-to-nearest-even to 8 significant bits
-    uint32_t u = __float_as_uint(r);
-    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
-    const float hi = __uint_as_float(u);
-    p[i] = __builtin_bit_cast(__bf16, (unsigned short)(u >> 16));
-    r -= hi;
-#else
-    p[i] = (__bf16)r;
+    p[i] = (__bf16)r;  // round to nearest even
     r -= (float)p[i];
-#endif
   }
 }
 
@@ -1824,9 +1155,6 @@ __device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&q)[NP], const bf16x8
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[a], x[ord - a], acc, 0, 0, 0);
   return acc;
 }
-#ifndef SVDJ_SPLIT_ACC
-#define SVDJ_SPLIT_ACC 1
-#endif
 
 template <int W, int NP>
 __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
@@ -1921,19 +1249,12 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
         bf16x8 q[NP];
 #pragma unroll
         for (int i = 0; i < NP; ++i) q[i] = Qf[i][ct][kb][lane];
-        if constexpr (SVDJ_SPLIT_ACC == 0) {
-          acc = mfma_split<NP, 0>(q, xs[kb], acc);
-        } else {
-          lo = mfma_split<NP, 1>(q, xs[kb], lo);
-          if constexpr (SVDJ_SPLIT_ACC == 1) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], acc, 0, 0, 0);
-          } else {
-            acc += __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], Mfma<float>::zero(),
-                                                           0, 0, 0);
-          }
-        }
+        // the high-order product in its own accumulator, the small terms in
+        // a second one (two chains remove the bias of a single chain)
+        lo = mfma_split<NP, 1>(q, xs[kb], lo);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], acc, 0, 0, 0);
       }
-      if constexpr (SVDJ_SPLIT_ACC != 0) acc += lo;
+      acc += lo;
       float* dst = ct * 32 < W ? xi + (size_t)(ct * 32) * ld : xj + (size_t)(ct * 32 - W) * ld;
 #pragma unroll
       for (int e = 0; e < 16; ++e)
@@ -1955,15 +1276,8 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // Gram: split-K over row chunks (>= 128 rows each), ~512 workgroups.
   // Many pairs per step want few chunks (every chunk is a slab the EVD sums:
   // 1-GPU 16384^2, W=64, 5.92 s at 512 vs 6.23 s at 2048).  With few pairs
-  // (many GPUs) the two chains' phase relation makes the optimum jump between
-  // 512 and 1024 from one kernel revision to the next (8-GPU rank plan,
-  // W=32: 80.9 / 67.0 ms per sweep before the EVD step unroll, 62 / 81 after;
-  // profiles/r2_stagger).
-  static const int gram_env = [] {
-    const char* e = getenv("SVDJ_GRAM_WG_TARGET");  // tuning experiments only
-    return e && atoi(e) > 0 ? atoi(e) : 0;
-  }();
-  const int gram_target = gram_env ? gram_env : 512;
+  // (many GPUs) 64-256 measured slower (8-GPU rank plan 65.5 -> 74-78 ms).
+  constexpr int gram_target = 512;
   int want = (gram_target + P - 1) / P;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
@@ -1976,15 +1290,11 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // workgroups costs more than the occupancy gains: 16384^2 rank plans
   // P=2/4/8 206.5/126.2/63.0 -> 203.5/114.5/59.8 ms per sweep, 8192^2 one GPU
   // 866 -> 799 ms, 32768x8192 (QR) 943 -> 888 ms; W = 32 (4096^2, fp64
-  // 5000^2) 2-3.5 % slower at 512 (tools/gpu_r2_awg2.sh / awg3.sh,
-  // profiles/r2_awg).  The split-bf16 applies (mma != 0) keep 2048: their
-  // larger Q images (32768x8192 bf16 with QR: 811 -> 847 ms at 512).
+  // 5000^2) 2-3.5 % slower at 512 (profiles/r2_awg).  The split-bf16 applies
+  // (mma != 0) keep 2048: their larger Q images (32768x8192 bf16 with QR:
+  // 811 -> 847 ms at 512).
   int total_rows = m_pad + n_v;
-  static const int wg_env = [] {
-    const char* e = getenv("SVDJ_APPLY_WG_TARGET");  // tuning experiments only
-    return e && atoi(e) > 0 ? atoi(e) : 0;
-  }();
-  const int wg_target = wg_env ? wg_env : (W == 64 && P < 64 && mma == 0 ? 512 : 2048);
+  const int wg_target = W == 64 && P < 64 && mma == 0 ? 512 : 2048;
   int rows = round_up((int)(((long)total_rows * P + wg_target - 1) / wg_target), 128);
   if (rows < 128) rows = 128;
   if (rows > 2048) rows = 2048;
@@ -2047,56 +1357,6 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   return 0;
 }
 
-// The LDS-staged cross Gram (fp32 W = 64), opt-in: SVDJ_GRAM_LDS=<ring depth
-// 2..4>.  Needs 16-byte aligned column starts and chunk rows a multiple of the
-// stage height.
-static int gram_lds_stages() {
-  static const int ns = [] {
-    const char* e = getenv("SVDJ_GRAM_LDS");
-    const int v = e ? atoi(e) : 0;
-    return v >= 2 && v <= 4 ? v : 0;
-  }();
-  return ns;
-}
-static void launch_gram_lds(int ns, dim3 grid, hipStream_t st, const float* A, int lda, int m_pad,
-                            const int32_t* pairs, int rows, float* slabs) {
-  if (ns == 2)
-    hipLaunchKernelGGL(gram_lds_kernel<2>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
-                       rows, slabs);
-  else if (ns == 3)
-    hipLaunchKernelGGL(gram_lds_kernel<3>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
-                       rows, slabs);
-  else
-    hipLaunchKernelGGL(gram_lds_kernel<4>, grid, dim3(kGramThreads), 0, st, A, lda, m_pad, pairs,
-                       rows, slabs);
-}
-template <typename T, int W>
-static bool gram_lds_ok(const Chain<T>& c) {
-  if constexpr (!(std::is_same<T, float>::value && W == 64)) {
-    (void)c;
-    return false;
-  } else {
-    return gram_lds_stages() && c.lda % 4 == 0 && (uintptr_t)c.A % 16 == 0 &&
-           c.g.grows % kGramLdsKT == 0 && c.m_pad % kGramLdsKT == 0;
-  }
-}
-
-// Register-resident bipartite EVD (fp32 W = 64): off by default (slower,
-// see evd_bip_reg_kernel), SVDJ_EVD_REG=1 selects it; svdj_set_evd_reg()
-// overrides both (tests run the two kernels in one process).
-static int g_evd_reg = -1;
-static bool evd_reg_enabled() {
-  static const bool env = [] {
-    const char* e = getenv("SVDJ_EVD_REG");
-    return e ? e[0] != '0' : SVDJ_EVD_REG_DEFAULT != 0;
-  }();
-  return g_evd_reg < 0 ? env : g_evd_reg != 0;
-}
-template <typename T, int W>
-static bool evd_reg_ok() {
-  return std::is_same<T, float>::value && W == 64 && evd_reg_enabled();
-}
-
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
 template <typename T, int W>
@@ -2114,19 +1374,12 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
     else
       hipLaunchKernelGGL((gram_kernel<T, W, GRAM_FULL>), dim3(c.P, c.g.gchunks),
                          dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
-  } else if (gram_lds_ok<T, W>(c)) {
-    launch_gram_lds(gram_lds_stages(), dim3(c.P, c.g.gchunks), c.st, (const float*)c.A, c.lda,
-                    c.m_pad, pr, c.g.grows, (float*)c.slabs);
   } else {
     hipLaunchKernelGGL((gram_kernel<T, W, GRAM_CROSS>), dim3(c.P, c.g.gchunks, XS),
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   }
   SVDJ_LAUNCH_CHECK();
-  if (mode == 2 && evd_reg_ok<T, W>())
-    hipLaunchKernelGGL(evd_bip_reg_kernel, dim3(c.P), dim3(1024), 0, c.st, pr, (const float*)c.slabs,
-                       c.g.gchunks, (float*)c.D, (float*)c.Qb[b], c.skipb[b], (float)tol, absmode,
-                       max_inner, metric);
-  else if (mode == 2)
+  if (mode == 2)
     hipLaunchKernelGGL((evd_kernel<T, W, EVD_BIP>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr,
                        0, c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode,
                        max_inner, metric);
@@ -2138,54 +1391,29 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
   return 0;
 }
 
-// part: 0 = A and V rows in one launch, 1 = A rows only, 2 = V rows only
-// (on stream st; the V rows are then addressed as the kernel's "A" region)
 template <typename T, int W>
-static int launch_apply(const Chain<T>& c, int s, int mma, int part = 0,
-                        hipStream_t st = nullptr) {
+static int launch_apply(const Chain<T>& c, int s, int mma) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
-  if (!st) st = c.st;
-  T* X = c.A;
-  int ldx = c.lda, xch = c.g.a_chunks, xrows = c.g.rows_a, xpad = c.m_pad;
-  T* Y = c.V;
-  int nv = c.V ? c.n_v : 0, ych = c.g.v_chunks;
-  if (part == 1) {
-    Y = nullptr;
-    nv = ych = 0;
-  } else if (part == 2) {
-    if (!c.V) return 0;
-    X = c.V;
-    ldx = c.ldv;
-    xch = c.g.v_chunks;
-    xrows = c.g.rows_v;
-    xpad = c.n_v;
-    Y = nullptr;
-    nv = ych = 0;
-  }
-  const dim3 grid(c.P, xch + ych);
+  const int nv = c.V ? c.n_v : 0, ych = c.V ? c.g.v_chunks : 0;
+  const dim3 grid(c.P, c.g.a_chunks + ych);
   if constexpr (sizeof(T) == 4) {
     if (mma == 1 || mma == 2) {
       if (mma == 1)
-        hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, st, X, ldx,
-                           xch, xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
+        hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
+                           pr, c.Qb[b], c.skipb[b]);
       else
-        hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, st, X, ldx,
-                           xch, xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
-      SVDJ_LAUNCH_CHECK();
-      return 0;
-    }
-    // 16-byte X loads: leading dimensions and base pointers 16-byte aligned
-    if (apply_ldsx_enabled() && ldx % 4 == 0 && (nv == 0 || c.ldv % 4 == 0) &&
-        ((uintptr_t)X | (uintptr_t)Y) % 16 == 0) {
-      hipLaunchKernelGGL((apply_ldsx_kernel<W>), grid, dim3(4 * W), 0, st, X, ldx, xch, xrows,
-                         xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
+        hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
+                           pr, c.Qb[b], c.skipb[b]);
       SVDJ_LAUNCH_CHECK();
       return 0;
     }
   }
-  hipLaunchKernelGGL((apply_kernel<T, W>), grid, dim3(apply_threads<T, W>()), 0, st, X, ldx, xch,
-                     xrows, xpad, Y, c.ldv, c.g.rows_v, nv, pr, c.Qb[b], c.skipb[b]);
+  hipLaunchKernelGGL((apply_kernel<T, W>), grid, dim3(apply_threads<T, W>()), 0, c.st, c.A, c.lda,
+                     c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv, pr, c.Qb[b],
+                     c.skipb[b]);
   SVDJ_LAUNCH_CHECK();
   return 0;
 }
@@ -2247,80 +1475,14 @@ static hipEvent_t* stagger_events(hipStream_t rec, hipStream_t wait, int& n) {
   return r->ev;
 }
 
-// ---- deferred V rotation (SVDJ_VSTREAM=1).  The next step's Gram reads A
-// only, so a chain can run apply(V rows, s) on a side stream while its
-// gram / EVD of step s+1 proceed: the side stream waits for EVD(s) (Q ready),
-// EVD(s+2) waits for apply(V, s) (it rewrites the same Q / skip buffer), and
-// the chain stream joins the side stream at the end of the call.
-static hipStream_t side_stream(hipStream_t st) {
-  static std::mutex mu;
-  static std::vector<std::pair<hipStream_t, hipStream_t>> m;
-  std::lock_guard<std::mutex> lock(mu);
-  for (auto& x : m)
-    if (x.first == st) return x.second;
-  int sdev = 0, cur = 0;
-  if (hipStreamGetDevice(st, &sdev) != hipSuccess || hipGetDevice(&cur) != hipSuccess) return nullptr;
-  if (sdev != cur && hipSetDevice(sdev) != hipSuccess) return nullptr;
-  hipStream_t v = nullptr;
-  const bool ok = hipStreamCreateWithFlags(&v, hipStreamNonBlocking) == hipSuccess;
-  if (sdev != cur) (void)hipSetDevice(cur);
-  if (!ok) return nullptr;
-  m.push_back({st, v});
-  return v;
-}
-static bool vstream_on() {
-  static const bool on = [] {
-    const char* e = getenv("SVDJ_VSTREAM");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-template <typename T>
-struct VSide {
-  hipStream_t vst = nullptr;
-  hipEvent_t *qready = nullptr, *vdone = nullptr;
-  int nq = 0, nv = 0;
-  bool init(const Chain<T>& c) {
-    if (!c.V || !vstream_on()) return true;
-    vst = side_stream(c.st);
-    if (!vst) return false;
-    qready = stagger_events(c.st, vst, nq);
-    vdone = stagger_events(vst, c.st, nv);
-    return qready && vdone;
-  }
-};
-// gram + EVD of step s, then the apply (A rows on the chain stream, V rows
-// on the side stream when it is enabled)
-template <typename T, int W>
-static int step_deferred(const Chain<T>& c, VSide<T>& v, int s, double tol, int absmode,
-                         int max_inner, uint32_t* metric, int mma, hipEvent_t after_evd) {
-  if (v.vst && s >= 2 && hipStreamWaitEvent(c.st, v.vdone[(s - 2) % v.nv], 0) != hipSuccess)
-    return -100;
-  int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric);
-  if (rc) return rc;
-  if (after_evd && hipEventRecord(after_evd, c.st) != hipSuccess) return -100;
-  if (!v.vst) return launch_apply<T, W>(c, s, mma);
-  if (hipEventRecord(v.qready[s % v.nq], c.st) != hipSuccess) return -100;
-  rc = launch_apply<T, W>(c, s, mma, 1);
-  if (rc) return rc;
-  if (hipStreamWaitEvent(v.vst, v.qready[s % v.nq], 0) != hipSuccess) return -100;
-  rc = launch_apply<T, W>(c, s, mma, 2, v.vst);
-  if (rc) return rc;
-  return hipEventRecord(v.vdone[s % v.nv], v.vst) == hipSuccess ? 0 : -100;
-}
-template <typename T>
-static int join_side(const Chain<T>& c, const VSide<T>& v) {
-  if (!v.vst || c.steps <= 0) return 0;
-  return hipStreamWaitEvent(c.st, v.vdone[(c.steps - 1) % v.nv], 0) == hipSuccess ? 0 : -100;
-}
-
-// Two independent chains on two streams, staggered: chain B's step s starts
-// when chain A's EVD of step s has finished.  Issued separately the chains
-// run in lockstep (identical steps): both EVDs -- one workgroup per pair,
-// most CUs idle -- overlap each other, and so do both applies.  Staggered,
-// B's gram/EVD run under A's apply and A's next gram/EVD under B's apply,
-// which matters when the per-GPU work is small (many GPUs): the EVD latency
-// is then the critical path (tools/gpu_latency_sim.sh, tools/trace_gaps.py).
+// Two independent chains on two streams, staggered (SolverConfig.stagger):
+// chain B's step s starts when chain A's EVD of step s has finished, so B's
+// gram/EVD run under A's apply and A's next gram/EVD under B's apply.  Round
+// 1 needed this; since the bipartite EVD and the round-2 apply geometry,
+// independent issue (one svdj_block_steps per chain) is faster (8-GPU rank
+// plan 59.4 -> 57.5 ms per sweep), so it is off by default.  A symmetric
+// stagger, four chains in a cascade and hipGraph replay of this issue were
+// measured slower in round 2 and removed (git history, profiles/r2_*).
 template <typename T, int W>
 static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int absmode,
                           int max_inner, uint32_t* metric, int mma) {
@@ -2330,50 +1492,23 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
     set_error("stagger events unavailable");
     return -100;
   }
-  // SVDJ_STAGGER_SYM=1 (experiment, off): chain A's step s+1 also waits for
-  // chain B's EVD of step s, so the EVDs strictly alternate.  Measured slower
-  // everywhere (8-GPU rank plan W=64 64.5 -> 80.0 ms per sweep, one GPU
-  // 16384^2 5.74 -> 6.02 s, profiles/r2_stagger): the one-sided stagger
-  // lets the faster chain run ahead.
-  static const bool sym = [] {
-    const char* e = getenv("SVDJ_STAGGER_SYM");
-    return e && e[0] == '1';
-  }();
-  int nr = 0;
-  hipEvent_t* evr = sym ? stagger_events(b.st, a.st, nr) : nullptr;
-  if (sym && !evr) {
-    set_error("stagger events unavailable");
-    return -100;
-  }
-  VSide<T> va, vb;
-  if (!va.init(a) || !vb.init(b)) {
-    set_error("side stream / events unavailable");
-    return -100;
-  }
   const int n = a.steps > b.steps ? a.steps : b.steps;
   for (int s = 0; s < n; ++s) {
     int rc = 0;
     if (s < a.steps) {
-      if (sym && s > 0 && s - 1 < b.steps && hipStreamWaitEvent(a.st, evr[(s - 1) % nr], 0) != hipSuccess)
-        rc = -100;
-      if (!rc)
-        rc = step_deferred<T, W>(a, va, s, tol, absmode, max_inner, metric, mma,
-                                 s < b.steps ? ev[s % ne] : nullptr);
+      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
+      if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
+      if (!rc) rc = launch_apply<T, W>(a, s, mma);
     }
     if (!rc && s < b.steps) {
       if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
-      if (!rc)
-        rc = step_deferred<T, W>(b, vb, s, tol, absmode, max_inner, metric, mma,
-                                 sym && s + 1 < a.steps ? evr[s % nr] : nullptr);
+      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric);
+      if (!rc) rc = launch_apply<T, W>(b, s, mma);
     }
     if (rc) {
       if (rc == -100) set_error("stagger event record/wait failed");
       return rc;
     }
-  }
-  if (join_side(a, va) || join_side(b, vb)) {
-    set_error("side stream join failed");
-    return -100;
   }
   return 0;
 }
@@ -2381,17 +1516,6 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
 }  // namespace svdj
 
 using namespace svdj;
-
-#ifdef SVDJ_EVD_PROFILE
-extern "C" int svdj_debug_evd_profile(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_evd_prof), sizeof(g_evd_prof)) != hipSuccess) return -1;
-  if (reset) {
-    static const unsigned long long z[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_evd_prof), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 
 extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
   return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);
@@ -2411,74 +1535,6 @@ static int check_dims(int m_pad, int lda, const void* V, int n_v, int ldv, int m
     return -2;
   }
   return 0;
-}
-
-// N independent chains (disjoint blocks) on N streams, staggered in a
-// cascade: chain c's step s starts when chain c-1's EVD of step s is done.
-// With few pairs per step (many GPUs) every chain's gram -> EVD -> apply is
-// latency-bound; four half-size chains keep twice as many of those latency
-// chains in flight as two (parallel/pipeline.py sweep_plan(chains=4)).
-template <typename T, int W>
-static int block_stepsN_t(const Chain<T>* ch, int nch, double tol, int absmode, int max_inner,
-                          uint32_t* metric, int mma) {
-  // SVDJ_STAGGER_N: 0 = cascade (c waits on c-1), 1 = pairs (odd c waits on
-  // c-1: (0,1), (2,3) staggered as two block_steps2), 2 = none
-  static const int smode = [] {
-    const char* e = getenv("SVDJ_STAGGER_N");
-    return e ? atoi(e) : 1;
-  }();
-  auto waits = [&](int c) { return c > 0 && (smode == 0 || (smode == 1 && (c & 1))); };
-  hipEvent_t* ev[8] = {};
-  int ne[8] = {};
-  for (int c = 0; c + 1 < nch; ++c) {
-    ev[c] = stagger_events(ch[c].st, ch[c + 1].st, ne[c]);
-    if (!ev[c]) {
-      set_error("stagger events unavailable");
-      return -100;
-    }
-  }
-  int n = 0;
-  for (int c = 0; c < nch; ++c) n = ch[c].steps > n ? ch[c].steps : n;
-  for (int s = 0; s < n; ++s) {
-    for (int c = 0; c < nch; ++c) {
-      const Chain<T>& x = ch[c];
-      if (s >= x.steps) continue;
-      int rc = 0;
-      if (waits(c) && s < ch[c - 1].steps &&
-          hipStreamWaitEvent(x.st, ev[c - 1][s % ne[c - 1]], 0) != hipSuccess)
-        rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(x, s, tol, absmode, max_inner, metric);
-      if (!rc && c + 1 < nch && waits(c + 1) && s < ch[c + 1].steps &&
-          hipEventRecord(ev[c][s % ne[c]], x.st) != hipSuccess)
-        rc = -100;
-      if (!rc) rc = launch_apply<T, W>(x, s, mma);
-      if (rc) {
-        if (rc == -100) set_error("stagger event record/wait failed");
-        return rc;
-      }
-    }
-  }
-  return 0;
-}
-
-template <typename T, int W>
-static int stepsN_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D, int nch,
-                           const int32_t* const* pairs, const int* P, const int* steps,
-                           const int32_t* const* modes, void* const* ws, const size_t* ws_bytes,
-                           void* const* streams, double tol, int absmode, int max_inner,
-                           uint32_t* metric, int mma) {
-  Chain<T> ch[8];
-  for (int c = 0; c < nch; ++c) {
-    for (int d = 0; d < c; ++d)
-      if (ws[d] == ws[c] || streams[d] == streams[c]) {
-        set_error("chains need distinct workspaces and streams");
-        return -2;
-      }
-    int rc = chain_init<T, W>(ch[c], m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs[c], P[c],
-                              steps[c], modes[c], ws[c], ws_bytes[c], mma, (hipStream_t)streams[c]);
-    if (rc) return rc;
-  }
-  return block_stepsN_t<T, W>(ch, nch, tol, absmode, max_inner, metric, mma);
 }
 
 template <typename T, int W>
@@ -2539,138 +1595,15 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
                    nullptr, 0, nullptr);
 }
 
-// ---- hipGraph replay of a staggered two-chain issue.  A sweep issues the
-// same block_steps2 calls every time (same pairs, workspaces, metric, modes):
-// the first call with a given argument set is captured from both streams
-// into one graph (fork / join events), later calls launch the graph -- one
-// host call instead of 3 launches + 2 event operations per step and chain.
-// Off by default (SVDJ_GRAPH=1 enables it): the eager issue keeps ahead of
-// the GPU at every size measured, and the replay was slower (2048^2 48 ->
-// 55 ms, 8-GPU rank plan 63 -> 72 ms per sweep; profiles/r2_graph).
-namespace {
-struct Steps2Graph {
-  std::vector<long long> key;
-  hipGraphExec_t exec = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, pre = nullptr, post = nullptr;
-};
-std::mutex g_graph_mu;
-std::vector<Steps2Graph*> g_graphs;  // FIFO, at most kGraphCache entries
-constexpr size_t kGraphCache = 64;
-
-void destroy_graph(Steps2Graph* g) {
-  if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  for (hipEvent_t e : {g->fork, g->join, g->pre, g->post})
-    if (e) (void)hipEventDestroy(e);
-  delete g;
-}
-}  // namespace
-
 extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                  int ldv, void* D, const int32_t* pairs, int P, int steps,
                                  const int32_t* modes, void* ws, size_t ws_bytes, void* stream,
                                  const int32_t* pairs2, int P2, int steps2, const int32_t* modes2,
                                  void* ws2, size_t ws2_bytes, void* stream2, double tol,
                                  int tol_mode, int max_inner, uint32_t* metric, int mma) {
-  auto eager = [&]() {
-    return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
-                     tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2,
-                     modes2, ws2, ws2_bytes, stream2);
-  };
-  static const bool use_graph = [] {
-    const char* e = getenv("SVDJ_GRAPH");
-    return e && e[0] == '1';
-  }();
-  if (!use_graph || !pairs2 || P <= 0 || P2 <= 0 || steps <= 0 || steps2 <= 0 || stream == stream2)
-    return eager();
-  hipStream_t sa = (hipStream_t)stream, sb = (hipStream_t)stream2;
-  std::vector<long long> key = {dtype, W, m_pad, (long long)A, lda, (long long)V, n_v, ldv,
-                                (long long)D, (long long)pairs, P, steps, (long long)ws,
-                                (long long)ws_bytes, (long long)stream, (long long)pairs2, P2,
-                                steps2, (long long)ws2, (long long)ws2_bytes, (long long)stream2,
-                                tol_mode, max_inner, (long long)metric, mma};
-  long long tbits;
-  memcpy(&tbits, &tol, sizeof(tbits));
-  key.push_back(tbits);
-  for (int i = 0; i < steps; ++i) key.push_back(modes ? modes[i] : 0);
-  for (int i = 0; i < steps2; ++i) key.push_back(modes2 ? modes2[i] : 0);
-  std::lock_guard<std::mutex> lock(g_graph_mu);
-  Steps2Graph* g = nullptr;
-  for (Steps2Graph* x : g_graphs)
-    if (x->key == key) g = x;
-  if (!g) {
-    // events of the stagger ring are created before capture begins
-    int ne = 0;
-    if (!stagger_events(sa, sb, ne)) {
-      set_error("stagger events unavailable");
-      return -100;
-    }
-    g = new Steps2Graph;
-    g->key = key;
-    bool ok = true;
-    for (hipEvent_t* e : {&g->fork, &g->join, &g->pre, &g->post})
-      ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
-    hipGraph_t graph = nullptr;
-    int rc = ok ? 0 : -100;
-    if (!rc && hipStreamBeginCapture(sa, hipStreamCaptureModeThreadLocal) != hipSuccess) rc = -100;
-    if (!rc) {
-      // fork: stream b joins the capture; join: a waits for b's last node
-      if (hipEventRecord(g->fork, sa) != hipSuccess || hipStreamWaitEvent(sb, g->fork, 0) != hipSuccess)
-        rc = -100;
-      if (!rc) rc = eager();
-      if (hipEventRecord(g->join, sb) != hipSuccess || hipStreamWaitEvent(sa, g->join, 0) != hipSuccess)
-        rc = rc ? rc : -100;
-      if (hipStreamEndCapture(sa, &graph) != hipSuccess) rc = rc ? rc : -100;
-    }
-    if (!rc && hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0) != hipSuccess) rc = -100;
-    if (graph) (void)hipGraphDestroy(graph);
-    if (rc) {
-      destroy_graph(g);
-      if (rc == -100) set_error("block_steps2 graph capture failed");
-      return rc;
-    }
-    if (g_graphs.size() >= kGraphCache) {
-      destroy_graph(g_graphs.front());
-      g_graphs.erase(g_graphs.begin());
-    }
-    g_graphs.push_back(g);
-  }
-  // the graph runs after everything already on either stream, and work
-  // issued later on either stream runs after the graph
-  if (hipEventRecord(g->pre, sb) != hipSuccess || hipStreamWaitEvent(sa, g->pre, 0) != hipSuccess ||
-      hipGraphLaunch(g->exec, sa) != hipSuccess || hipEventRecord(g->post, sa) != hipSuccess ||
-      hipStreamWaitEvent(sb, g->post, 0) != hipSuccess) {
-    set_error("block_steps2 graph launch failed");
-    return -100;
-  }
-  return 0;
-}
-
-extern "C" int svdj_block_stepsN(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
-                                 int ldv, void* D, int nchains, const int32_t* const* pairs,
-                                 const int* P, const int* steps, const int32_t* const* modes,
-                                 void* const* ws, const size_t* ws_bytes, void* const* streams,
-                                 double tol, int tol_mode, int max_inner, uint32_t* metric,
-                                 int mma) {
-  int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
-  if (rc) return rc;
-  if (tol_mode != 0 && tol_mode != 1) {
-    set_error("bad tol_mode %d (0 relative, 1 absolute)", tol_mode);
-    return -2;
-  }
-  if (nchains < 1 || nchains > 8) {
-    set_error("nchains %d (1..8)", nchains);
-    return -2;
-  }
-#define SVDJ_STEPSN_ARGS                                                                      \
-  m_pad, A, lda, V, n_v, ldv, D, nchains, pairs, P, steps, modes, ws, ws_bytes, streams, tol, \
-      tol_mode, max_inner, metric, mma
-  if (dtype == 0 && W == 32) return stepsN_dispatch<float, 32>(SVDJ_STEPSN_ARGS);
-  if (dtype == 0 && W == 64) return stepsN_dispatch<float, 64>(SVDJ_STEPSN_ARGS);
-  if (dtype == 1 && W == 32) return stepsN_dispatch<double, 32>(SVDJ_STEPSN_ARGS);
-  if (dtype == 1 && W == 64) return stepsN_dispatch<double, 64>(SVDJ_STEPSN_ARGS);
-#undef SVDJ_STEPSN_ARGS
-  set_error("unsupported (dtype=%d, W=%d); supported: W in {32, 64}", dtype, W);
-  return -3;
+  return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
+                   tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2,
+                   modes2, ws2, ws2_bytes, stream2);
 }
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
@@ -2734,14 +1667,9 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   return rc ? rc : sweeps;
 }
 
-// Test/diagnostic hook: X <- X Q for ONE column-block pair (blocks 0 and 1 of
-// X, 2W columns with leading dimension ld, rows padded to SVDJ_ROW_ALIGN),
-// Q row-major 2W x 2W on the device, with the given matrix-core mode.
 // Cross Gram alone (tests / kernel A/B): slabs (P x nchunk x W x W) of
 // A_bi^T A_bj for the device pair list, with the given row chunking.
-// kernel: 0 = register-fragment gram_kernel, 2..4 = LDS-staged with that
-// ring depth (fp32 W = 64).
-extern "C" int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int lda, int m_pad,
+extern "C" int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_pad,
                                const int32_t* pairs, int P, int rows_per_chunk, void* slabs,
                                void* stream) {
   if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad || P <= 0 || rows_per_chunk <= 0 ||
@@ -2751,14 +1679,7 @@ extern "C" int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int 
   }
   hipStream_t st = (hipStream_t)stream;
   const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
-  if (kernel >= 2) {  // LDS-staged, ring depth `kernel`
-    if (dtype != 0 || W != 64 || lda % 4 || (uintptr_t)A % 16 || kernel > 4) {
-      set_error("svdj_gram_cross: LDS kernel needs fp32, W=64, 16-byte aligned columns, depth 2..4");
-      return -3;
-    }
-    launch_gram_lds(kernel, dim3(P, nchunk), st, (const float*)A, lda, m_pad, pairs, rows_per_chunk,
-                    (float*)slabs);
-  } else if (dtype == 0 && W == 64) {
+  if (dtype == 0 && W == 64) {
     hipLaunchKernelGGL((gram_kernel<float, 64, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
                        0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
   } else if (dtype == 0 && W == 32) {
@@ -2776,13 +1697,9 @@ extern "C" int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int 
   return 0;
 }
 
-// Select the bipartite EVD kernel for fp32 W = 64: 1 register-resident,
-// 0 LDS position-space, -1 back to the SVDJ_EVD_REG / build default.
-extern "C" int svdj_set_evd_reg(int on) {
-  g_evd_reg = on < 0 ? -1 : (on ? 1 : 0);
-  return 0;
-}
-
+// Test/diagnostic hook: X <- X Q for ONE column-block pair (blocks 0 and 1 of
+// X, 2W columns with leading dimension ld, rows padded to SVDJ_ROW_ALIGN),
+// Q row-major 2W x 2W on the device, with the given matrix-core mode.
 extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q,
                             void* stream) {
   if (rows <= 0 || rows % SVDJ_ROW_ALIGN || ld < rows) {
@@ -2811,15 +1728,7 @@ extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld
   else if (dtype == 0 && mma == 2 && W == 32)
     hipLaunchKernelGGL((apply_split_kernel<32, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
-  else if (dtype == 0 && mma == 0 && apply_ldsx_enabled() && (W == 32 || W == 64) &&
-           ld % 4 == 0 && (uintptr_t)X % 16 == 0) {
-    if (W == 64)
-      hipLaunchKernelGGL((apply_ldsx_kernel<64>), grid, dim3(256), 0, st, (float*)X, ld, chunks,
-                         rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
-    else
-      hipLaunchKernelGGL((apply_ldsx_kernel<32>), grid, dim3(128), 0, st, (float*)X, ld, chunks,
-                         rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
-  } else if (dtype == 0 && mma == 0 && W == 64)
+  else if (dtype == 0 && mma == 0 && W == 64)
     hipLaunchKernelGGL((apply_kernel<float, 64>), grid, dim3(apply_threads<float, 64>()), 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
   else if (dtype == 0 && mma == 0 && W == 32)

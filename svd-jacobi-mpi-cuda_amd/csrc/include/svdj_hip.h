@@ -87,16 +87,6 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
                       double tol, int tol_mode, int max_inner_sweeps,
                       uint32_t* metric, int mma);
 
-// N (1..8) independent chains on N streams with their own workspaces,
-// staggered in a cascade: chain c's step s starts when chain c-1's EVD of
-// step s is done.  Arrays are indexed by chain; modes are host arrays.
-int svdj_block_stepsN(int dtype, int W, int m_pad, void* A, int lda, void* V,
-                      int n_v, int ldv, void* D, int nchains,
-                      const int32_t* const* pairs, const int* P, const int* steps,
-                      const int32_t* const* modes, void* const* workspace,
-                      const size_t* ws_bytes, void* const* streams, double tol,
-                      int tol_mode, int max_inner_sweeps, uint32_t* metric, int mma);
-
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
 // step, 1 = bipartite EVD in the cross steps (mode 2).  Returns sweeps, <0 on
@@ -107,12 +97,13 @@ int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      size_t ws_bytes, uint32_t* metric, double* hist,
                      int mma, void* stream);
 
-// Diagnostic hook: X <- X Q for one pair of column blocks (X = 2W columns,
-// leading dimension ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major
-// 2W x 2W on the device, with matrix-core mode `mma` (as svdj_block_steps).
-int svdj_set_evd_reg(int on);
-int svdj_gram_cross(int dtype, int W, int kernel, const void* A, int lda, int m_pad,
+// Diagnostic hooks.  Cross Gram slabs (P x nchunk x W x W) of A_bi^T A_bj
+// for a device pair list with the given row chunking (fp32).
+int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_pad,
                     const int32_t* pairs, int P, int rows_per_chunk, void* slabs, void* stream);
+// X <- X Q for one pair of column blocks (X = 2W columns, leading dimension
+// ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major 2W x 2W on the
+// device, with matrix-core mode `mma` (as svdj_block_steps).
 int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const void* Q, void* stream);
 
 // ---------------------------------------------------------------------------

@@ -93,8 +93,7 @@ def hip_lib():
             return _hip
         import torch  # noqa: F401  -- load torch's HIP runtime first (shared soname)
 
-        override = os.environ.get("SVDJ_HIP_LIB")  # A/B variants built by tools/
-        path = Path(override) if override else _ensure_built("hip")
+        path = _ensure_built("hip")
         try:
             lib = C.CDLL(str(path))
         except OSError as e:  # pragma: no cover - GPU box only
@@ -116,18 +115,12 @@ def hip_lib():
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
               c_int, c_int, c_i32_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_int,
               c_i32_p, c_void_p, c_size_t, c_void_p, c_double, c_int, c_int, c_void_p, c_int])
-        _sig(lib, "svdj_block_stepsN", c_int,
-             [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
-              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_double,
-              c_int, c_int, c_void_p, c_int])
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
               c_void_p])
-        _sig(lib, "svdj_set_evd_reg", c_int, [c_int])
         _sig(lib, "svdj_gram_cross", c_int,
-             [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-              c_void_p])
+             [c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_apply_q", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,

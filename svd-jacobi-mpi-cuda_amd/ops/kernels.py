@@ -294,60 +294,19 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
         mma_code(mma, At.dtype)), "block_steps2")
 
 
-def block_steps_multi(At, Vt, D, m_pad, W, tol, max_inner, metric, chains, mma="native",
-                      pool: dict | None = None, tol_mode="relative", inner_order="cyclic"):
-    """N independent chains of block steps (disjoint blocks), staggered in a
-    cascade (svdj_block_stepsN): ``chains`` is a list of ``(pairs, modes,
-    ws_slot, stream)`` as for block_steps2.  Two chains use block_steps2."""
-    if len(chains) == 2:
-        return block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chains[0], chains[1],
-                            mma, pool, tol_mode, inner_order)
-    if not At.is_cuda:
-        for pairs, modes, slot, _ in chains:
-            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool,
-                        tol_mode, inner_order)
-        return
-    _check_layout(At, m_pad)
-    check_block(At.dtype, W)
-    n = len(chains)
-    pr, Ps, st, md, wsp, wsb, sts = [], [], [], [], [], [], []
-    keep = []
-    for pairs, modes, slot, stream in chains:
-        steps, P = int(pairs.shape[0]), int(pairs.shape[1])
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool)
-        m_arr = (C.c_int32 * max(steps, 1))(*step_modes(modes, inner_order))
-        keep.append(m_arr)
-        pr.append(pairs.data_ptr())
-        Ps.append(P)
-        st.append(steps)
-        md.append(C.cast(m_arr, C.c_void_p).value)
-        wsp.append(ws.data_ptr())
-        wsb.append(ws.numel())
-        sts.append(stream.cuda_stream)
-    vp = C.c_void_p * n
-    n_v = Vt.shape[1] if Vt is not None else 0
-    ldv = Vt.stride(0) if Vt is not None else 0
-    hip_check(hip_lib().svdj_block_stepsN(
-        dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D), n,
-        vp(*pr), (C.c_int * n)(*Ps), (C.c_int * n)(*st), vp(*md), vp(*wsp),
-        (C.c_size_t * n)(*wsb), vp(*sts), float(tol), tol_mode_code(tol_mode), int(max_inner),
-        _ptr(metric), mma_code(mma, At.dtype)), "block_steps_multi")
-
-
-def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int, rows_per_chunk: int,
-               kernel: str = "lds", depth: int = 4) -> torch.Tensor:
+def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
+               rows_per_chunk: int) -> torch.Tensor:
     """Cross Gram A_bi^T A_bj of every (bi, bj) in ``pairs`` (P, 2) on the
     device, split over row chunks as in a block step; returns the chunk slabs
-    (P, nchunk, W, W).  ``kernel``: "lds" (LDS-staged, fp32 W=64, ring of
-    ``depth`` stages) or "reg"."""
+    (P, nchunk, W, W)."""
     _check_layout(At, m_pad)
     pairs = pairs.to(torch.int32).contiguous().to(At.device)
     P = pairs.shape[0]
     nchunk = -(-m_pad // rows_per_chunk)
     slabs = torch.empty(P, nchunk, W, W, dtype=At.dtype, device=At.device)
-    hip_check(hip_lib().svdj_gram_cross(dtype_code(At.dtype), W, depth if kernel == "lds" else 0,
-                                        _ptr(At), At.stride(0), m_pad, _ptr(pairs), P,
-                                        rows_per_chunk, _ptr(slabs), _stream(At)), "gram_cross")
+    hip_check(hip_lib().svdj_gram_cross(dtype_code(At.dtype), W, _ptr(At), At.stride(0), m_pad,
+                                        _ptr(pairs), P, rows_per_chunk, _ptr(slabs), _stream(At)),
+              "gram_cross")
     return slabs
 
 
@@ -404,7 +363,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
 __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
-    "block_workspace", "block_steps", "block_steps2", "block_steps_multi", "block_solve", "check_block", "MMA_CODES", "mma_code",
+    "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",
     "gram_cross",
 ]

@@ -50,6 +50,9 @@ class DistributedBlockJacobi(Solver):
 
     def __init__(self, config: SolverConfig | None = None, comm: Communicator | None = None):
         super().__init__(config)
+        if self.config.chains not in (1, 2):
+            raise ValueError(f"SolverConfig.chains must be 1 (blocking exchange) or 2 "
+                             f"(pipelined), got {self.config.chains}")
         self.comm = comm or Communicator()
         self._ws = {}  # this solver's kernel workspaces (never shared with another solver)
 
@@ -59,10 +62,8 @@ class DistributedBlockJacobi(Solver):
         W = self.config.block or choose_block(dtype, max(n // max(P, 1), 1), m)
         K.check_block(dtype, W)
         # pipelined sweeps split super-blocks in halves: k = B/W must be even
-        # pipelined sweeps split super-blocks in parts (halves / quarters):
-        # k = B/W must be a multiple of the part count
-        parts = self.config.chains if self.config.chains in (2, 4) else 1
-        q = 2 * max(parts, 1) * P * W
+        parts = 2 if self.config.chains == 2 else 1
+        q = 2 * parts * P * W
         ncols = round_up(max(n, q), q)
         B = ncols // (2 * P)
         return {"P": P, "W": W, "ncols": ncols, "B": B, "k": B // W, "m_pad": pad_rows(m),
@@ -230,9 +231,9 @@ class DistributedBlockJacobi(Solver):
         P, W, B, k, m_pad, n_v, ncols = (geo[x] for x in ("P", "W", "B", "k", "m_pad", "n_v", "ncols"))
         g = comm.rank
         tour = tournament(P)
-        pipelined = cfg.chains >= 2
+        pipelined = cfg.chains == 2
         if pipelined:
-            splan = sweep_plan(P, k, tour.xslot[:, g], chains=cfg.chains)
+            splan = sweep_plan(P, k, tour.xslot[:, g])
         else:
             plans = distributed_sweep_plan(P, k)
             dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
@@ -293,19 +294,13 @@ class DistributedBlockJacobi(Solver):
                                mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                                inner_order=cfg.inner_order)
 
-            def run_multi(chains):
-                K.block_steps_multi(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, chains,
-                                    mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                                    inner_order=cfg.inner_order)
-
             if not cfg.stagger:
-                run_pair = run_multi = None
+                run_pair = None
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
                 if pipelined:
-                    t_comm += ex.run(splan, run_steps, phys, run_pair,
-                                     run_multi if splan.parts > 2 else None)
+                    t_comm += ex.run(splan, run_steps, phys, run_pair)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:
@@ -361,7 +356,7 @@ class DistributedBlockJacobi(Solver):
         key = str(dev)
         cache = self.__dict__.setdefault("_streams", {})
         if key not in cache:
-            cache[key] = [torch.cuda.Stream(dev) for _ in range(max(2, self.config.chains))]
+            cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
         return cache[key]
 
     # ------------------------------------------------------- data movement

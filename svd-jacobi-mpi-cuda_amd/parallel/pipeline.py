@@ -80,12 +80,11 @@ def _bipartite(xs: list, ys: list) -> np.ndarray:
 
 def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2) -> SweepPlan:
     """Items of one sweep.  ``xslot[r]`` is the slot replaced before round r
-    (r >= 1), as produced by schedule.tournament.  ``chains=4``: quarters
-    instead of halves (sweep_plan4)."""
-    if chains == 4:
-        return sweep_plan4(P, k, xslot)
+    (r >= 1), as produced by schedule.tournament.  (Four chains in quarters
+    were measured slower than two at every P in round 2 -- 8-GPU plan 64 ->
+    84-88 ms per sweep -- and removed.)"""
     if chains != 2:
-        raise ValueError(f"pipelined sweep: 2 or 4 chains, got {chains}")
+        raise ValueError(f"pipelined sweep: 2 chains, got {chains}")
     if k < 2 or k % 2:
         raise ValueError(f"pipelined sweep needs an even block count per super-block, got {k}")
     plan = SweepPlan(P, k)
@@ -115,58 +114,10 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2) -> SweepPlan:
     return plan
 
 
-def sweep_plan4(P: int, k: int, xslot: np.ndarray) -> SweepPlan:
-    """Four chains: every super-block is four quarters q0..q3 (k/4 blocks).
-
-    Round 0, per slot s (chains 2s, 2s+1):  RR(q0 q1) || RR(q2 q3)   [first
-    step full], then q0 x q2 || q1 x q3, then q0 x q3 || q1 x q2.
-    Every round:  four phases t = 0..3 of I_c x S_(c+t)%4 on chain c (a
-    Latin square: each phase touches every quarter once).  The four quarters
-    of the next outgoing slot are sent after the last phase, each as soon as
-    its own last user is done.  Each
-    chain step holds k/4 pairs instead of k/2: with few pairs per step (many
-    GPUs) four shorter latency chains are in flight instead of two."""
-    if k < 4 or k % 4:
-        raise ValueError(f"4-chain sweep needs k % 4 == 0 blocks per super-block, got {k}")
-    plan = SweepPlan(P, k, parts=4)
-    q, h = k // 4, k // 2
-    rr = round_robin(h)
-    rr_modes = [1] + [0] * (h - 2)
-    for s in range(2):
-        for hh in range(2):
-            plan.items.append(Task(f"rr{s}{hh}", rr + s * k + hh * h, rr_modes, 2 * s + hh,
-                                   ((s, 2 * hh), (s, 2 * hh + 1))))
-    for pa, pb, pc, pd in ((0, 2, 1, 3), (0, 3, 1, 2)):
-        for s in range(2):
-            plan.items.append(Task(f"w{s}.{pa}{pb}", _bipartite(_blocks(s, pa, k, 4),
-                                                                 _blocks(s, pb, k, 4)),
-                                   [0] * q, 2 * s, ((s, pa), (s, pb))))
-            plan.items.append(Task(f"w{s}.{pc}{pd}", _bipartite(_blocks(s, pc, k, 4),
-                                                                 _blocks(s, pd, k, 4)),
-                                   [0] * q, 2 * s + 1, ((s, pc), (s, pd))))
-    R = 2 * P - 1
-    for r in range(R):
-        inc = int(xslot[r]) if r > 0 else 0
-        stay = 1 - inc
-        nxt = int(xslot[r + 1]) if r + 1 < R else None
-        for t in range(4):
-            for c in range(4):
-                p = (c + t) % 4
-                plan.items.append(Task(f"r{r}.T{c}{p}", _bipartite(_blocks(inc, c, k, 4),
-                                                                  _blocks(stay, p, k, 4)),
-                                       [0] * q, c, ((inc, c), (stay, p))))
-        if nxt is not None:
-            # after every user is issued, in the same order on every GPU (the
-            # grouped send/recv of part j must match across ranks); each send
-            # still starts as soon as ITS part's last user is done
-            plan.items.extend(Send(r + 1, nxt, part) for part in range(4))
-    return plan
-
-
 def issue_groups(items: list, stagger: bool, max_group: int = 2) -> list:
     """The plan's items regrouped for issue: a Task, a Send, or a tuple of up
     to ``max_group`` tasks issued jointly as staggered chains
-    (ops.kernels.block_steps2 / block_steps_multi).
+    (ops.kernels.block_steps2).
 
     Greedy: a task is grouped with the following tasks (Sends in between are
     skipped) while each runs on a new stream, touches parts disjoint from the
@@ -202,39 +153,6 @@ def issue_groups(items: list, stagger: bool, max_group: int = 2) -> list:
         out.append(tuple(group) if len(group) > 1 else it)
         out.extend(sd for idx, sd in skipped if idx < last)
         i = last + 1
-    return out
-
-
-def _issue_groups_pairs(items: list, stagger: bool) -> list:
-    """The plan's items regrouped for issue: a Task, a Send, or a (Task, Task)
-    pair issued jointly as two staggered chains (ops.kernels.block_steps2).
-
-    A task is paired with the next task (at most one Send in between) when the
-    two run on different streams, touch disjoint halves, and the Send in
-    between concerns neither of the second task's halves; that Send is then
-    issued after the pair (it only waits on events of earlier users of its
-    half, so the delay is host-side only).  Pairs: rr0+rr1, T01+T10, and the
-    last round's T00+T11 / T01+T10; T11 of a round pairs with T00 of the next
-    round across the half-1 Send."""
-    out = []
-    i, n = 0, len(items)
-    while i < n:
-        it = items[i]
-        if stagger and isinstance(it, Task):
-            j = i + 1
-            while j < n and isinstance(items[j], Send):
-                j += 1
-            sends = items[i + 1:j]
-            if j < n and len(sends) <= 1:
-                b = items[j]
-                if (b.stream != it.stream and not set(b.halves) & set(it.halves)
-                        and all((x.slot, x.half) not in b.halves for x in sends)):
-                    out.append((it, b))
-                    out.extend(sends)
-                    i = j + 1
-                    continue
-        out.append(it)
-        i += 1
     return out
 
 
@@ -336,7 +254,7 @@ class PipelineExecutor:
             self.dev_pairs[i] = t
         return t
 
-    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None, run_multi=None) -> float:
+    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
         steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
         independent chains staggered, ``a``/``b`` = (pairs, modes, slot,
@@ -361,8 +279,7 @@ class PipelineExecutor:
         index = {id(it): i for i, it in enumerate(plan.items)}
         groups = self._groups.get(id(plan))
         if groups is None:
-            groups = issue_groups(plan.items, run_pair is not None,
-                                  max_group=plan.parts if run_multi is not None else 2)
+            groups = issue_groups(plan.items, run_pair is not None)
             self._groups[id(plan)] = groups
         for it in groups:
             if isinstance(it, Send):
@@ -392,9 +309,6 @@ class PipelineExecutor:
                 a, b = tasks
                 run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
                          (pairs[1], b.modes, b.stream, self.streams[b.stream]))
-            elif len(tasks) > 2:
-                run_multi([(pr, t.modes, t.stream, self.streams[t.stream])
-                           for pr, t in zip(pairs, tasks)])
             else:
                 with torch.cuda.stream(self.streams[tasks[0].stream]):
                     run_steps(pairs[0], tasks[0].modes, tasks[0].stream)

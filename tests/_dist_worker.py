@@ -15,9 +15,7 @@ def main():
     mode = sys.argv[5] if len(sys.argv) > 5 else "root"
     comm = Communicator(backend="gloo", device=torch.device("cpu"))
     cfg = svdj.SolverConfig(block=W, dtype=torch.float64, max_inner_sweeps=1,
-                            precondition="qr" if "qr" in mode else "none",
-                            chains=4 if mode.endswith("4ch") else 2)
-    mode = mode[:-3] if mode.endswith("4ch") else mode
+                            precondition="qr" if "qr" in mode else "none")
     solver = DistributedBlockJacobi(cfg, comm)
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=9)
     if mode == "roundtrip":  # reference test_local_matrix_distribution_* parity

@@ -39,17 +39,6 @@ def test_distributed_block_jacobi_gloo(world, m, n, tmp_path):
     assert rep["orth_u_fro"] < 1e-10 and rep["orth_v_fro"] < 1e-10, rep
 
 
-@pytest.mark.parametrize("world,m,n", [(1, 140, 128), (2, 300, 256), (4, 300, 256)])
-def test_distributed_four_chains_gloo(world, m, n, tmp_path):
-    """Four chains (super-blocks in quarters, pipeline.sweep_plan4): same
-    solution quality as the two-chain plan."""
-    rep = _run(world, m, n, 32, tmp_path, mode="root4ch")
-    assert rep["converged"] and rep["world"] == world
-    assert rep["residual_rel"] < 1e-12, rep
-    assert rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
-    assert rep["orth_u_fro"] < 1e-10 and rep["orth_v_fro"] < 1e-10, rep
-
-
 def test_distributed_generator_input(tmp_path):
     rep = _run(2, 150, 128, 32, tmp_path, mode="gen")
     assert rep["converged"] and rep["residual_rel"] < 1e-12, rep

@@ -322,31 +322,28 @@ def test_svd_end_to_end_bipartite(svdj, cuda, dtype):
     assert rep["orth_u_fro"] < ou and rep["orth_v_fro"] < ov, rep
 
 
-def test_block_steps_multi_chain_matches_sequential(svdj, cuda):
-    """svdj_block_stepsN: four chains on four streams, staggered in a cascade,
-    on disjoint blocks give bitwise the result of running the chains one
-    after the other on one stream."""
+def test_block_steps2_staggered_matches_sequential(svdj, cuda):
+    """svdj_block_steps2: two chains on two streams, chain B's step s waiting
+    for chain A's EVD of step s, on disjoint blocks give bitwise the result of
+    running the chains one after the other on one stream."""
     K = svdj.ops.kernels
-    W, nb, m, m_pad = 32, 16, 700, 768
+    W, nb, m, m_pad = 32, 8, 700, 768
     n = nb * W
     A0 = _rand_At(n, m_pad, m, torch.float32, cuda, seed=11)
     rr = svdj.parallel.schedule.round_robin(4)  # 3 steps x 2 pairs on 4 blocks
-    chains = []
-    streams = [torch.cuda.Stream(cuda) for _ in range(4)]
-    for c in range(4):
-        pairs = torch.from_numpy(rr + 4 * c).to(cuda)
-        chains.append((pairs, [1, 0, 0], c, streams[c]))
+    streams = [torch.cuda.Stream(cuda) for _ in range(2)]
+    chains = [(torch.from_numpy(rr + 4 * c).to(cuda), [1, 0, 0], c, streams[c]) for c in range(2)]
 
-    def run(multi):
+    def run(staggered):
         At = A0.clone()
         Vt = torch.zeros(n, n, dtype=torch.float32, device=cuda)
         K.set_identity(Vt, n)
         D = K.col_norms2(At, m_pad)
         metric = K.new_metric(cuda)
         torch.cuda.synchronize()
-        if multi:
-            K.block_steps_multi(At, Vt, D, m_pad, W, 1e-6, 1, metric, chains, pool={},
-                                inner_order="bipartite")
+        if staggered:
+            K.block_steps2(At, Vt, D, m_pad, W, 1e-6, 1, metric, chains[0], chains[1], pool={},
+                           inner_order="bipartite")
         else:
             for pairs, modes, slot, _ in chains:
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, 1e-6, 1, metric, slot, pool={},
@@ -360,78 +357,22 @@ def test_block_steps_multi_chain_matches_sequential(svdj, cuda):
     assert torch.equal(a1, a0) and torch.equal(v1, v0) and torch.equal(d1, d0)
 
 
+@pytest.mark.parametrize("W", [32, 64])
 @pytest.mark.parametrize("m,m_pad,rows", [(100, 128, 128), (500, 512, 128), (4000, 4096, 1024),
                                           (5000, 5120, 3072), (3000, 3072, 256)])
-def test_gram_cross_lds_matches_reference(svdj, cuda, m, m_pad, rows):
-    """LDS-staged cross Gram (fp32 W=64, glds ring) vs the fp64 torch product
-    and vs the register-fragment kernel: 1 to 24 stages per chunk (ring
-    prologue / drain paths), a short last chunk, and a leading dimension
-    larger than m_pad."""
+def test_gram_cross_matches_reference(svdj, cuda, W, m, m_pad, rows):
+    """Cross Gram kernel (fp32, register fragments, split over row chunks)
+    vs the fp64 torch product: one to many slabs per chunk, a short last
+    chunk, and a leading dimension larger than m_pad."""
     K = svdj.ops.kernels
-    W, nb = 64, 6
+    nb = 6
     ld = m_pad + 128
     At = torch.zeros(nb * W, ld, dtype=torch.float32, device=cuda)
     At[:, :m_pad] = _rand_At(nb * W, m_pad, m, torch.float32, cuda, seed=5)
     pairs = torch.tensor([[0, 5], [3, 1], [2, 4]], dtype=torch.int32)
-    reg = K.gram_cross(At, m_pad, pairs, W, rows, "reg").double().sum(1).cpu()
+    got = K.gram_cross(At, m_pad, pairs, W, rows).double().sum(1).cpu()
     A64 = At.double().cpu()[:, :m_pad]
-    for depth in (2, 3, 4):
-        lds = K.gram_cross(At, m_pad, pairs, W, rows, "lds", depth).double().sum(1).cpu()
-        for p, (bi, bj) in enumerate(pairs.tolist()):
-            ref = A64[bi * W:(bi + 1) * W] @ A64[bj * W:(bj + 1) * W].t()
-            scale = ref.abs().max().item()
-            assert (lds[p] - ref).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
-            assert (lds[p] - reg[p]).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
-
-
-@pytest.mark.parametrize("inner,converged_pair", [(1, False), (3, False), (1, True)])
-def test_evd_register_kernel_matches_lds_kernel(svdj, cuda, inner, converged_pair):
-    """fp32 W=64 bipartite cross step: the register-resident EVD
-    (evd_bip_reg_kernel) against the LDS position-space EVD on the same input
-    -- one and several inner sweeps, and a pair that is already converged
-    (skipped exactly: same rotation count, D untouched)."""
-    K = svdj.ops.kernels
-    lib = svdj.ops.hip_lib()
-    W, nb, m, m_pad = 64, 4, 700, 768
-    g = torch.Generator().manual_seed(11)
-    A64 = torch.zeros(nb * W, m_pad, dtype=torch.float64)
-    if converged_pair:
-        q, _ = torch.linalg.qr(torch.rand(m, 2 * W, generator=g, dtype=torch.float64))
-        q = q * torch.linspace(1, 4, 2 * W, dtype=torch.float64)
-        A64[0:W, :m], A64[3 * W:4 * W, :m] = q[:, :W].t(), q[:, W:].t()
-        todo = (1, 2)
-    else:
-        todo = range(nb)
-    for b in todo:
-        qb, _ = torch.linalg.qr(torch.rand(m, W, generator=g, dtype=torch.float64))
-        A64[b * W:(b + 1) * W, :m] = (qb * torch.linspace(1, 3, W, dtype=torch.float64)).t()
-    pairs = torch.tensor([[[0, 3], [1, 2]]], dtype=torch.int32, device=cuda)
-    out = {}
-    try:
-        for reg in (1, 0):
-            lib.svdj_set_evd_reg(reg)
-            At = A64.float().to(cuda)
-            Vt = torch.zeros(nb * W, 256, dtype=torch.float32, device=cuda)
-            K.set_identity(Vt, nb * W)
-            D = K.col_norms2(At, m_pad)
-            D0 = D.clone()
-            metric = K.new_metric(cuda)
-            K.block_steps(At, Vt, D, m_pad, pairs, W, [0], 1e-6, inner, metric,
-                          inner_order="bipartite")
-            out[reg] = (At.double().cpu(), Vt.double().cpu(), D.double().cpu(), D0.double().cpu(),
-                        K.read_metric(metric))
-    finally:
-        lib.svdj_set_evd_reg(-1)
-    (A1, V1, D1, D01, (mx1, n1)), (A0, V0, D0_, _, (mx0, n0)) = out[1], out[0]
-    assert n1 == n0 == (1 if converged_pair else 2)
-    assert math.isclose(mx1, mx0, rel_tol=1e-5)
-    # the LDS kernel keeps one copy of each symmetric entry, this one two
-    # (G(X_i, Y_j) and G(Y_j, X_i) rounded in different threads): rounding
-    # level apart after one sweep, drifting a little over several
-    tol = 2e-5 if inner == 1 else 1e-4
-    torch.testing.assert_close(A1, A0, rtol=tol, atol=tol)
-    torch.testing.assert_close(V1, V0, rtol=tol, atol=tol)
-    torch.testing.assert_close(D1, D0_, rtol=tol, atol=tol)
-    if converged_pair:
-        c03 = list(range(0, W)) + list(range(3 * W, 4 * W))
-        assert torch.equal(D1[c03], D01[c03])
+    for p, (bi, bj) in enumerate(pairs.tolist()):
+        ref = A64[bi * W:(bi + 1) * W] @ A64[bj * W:(bj + 1) * W].t()
+        scale = ref.abs().max().item()
+        assert (got[p] - ref).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)

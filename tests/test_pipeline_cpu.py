@@ -132,35 +132,6 @@ def test_native_block_rule_matches_python():
                     (dt, world, m, n)
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
-@pytest.mark.parametrize("k", [4, 8, 12])
-def test_four_chain_plan_covers_and_groups(P, k):
-    """sweep_plan4: every block pair meets once per sweep; every round's
-    tasks issue as groups of four disjoint chains; the four quarter sends of
-    a round come in the same order on every GPU."""
-    tour = schedule.tournament(P)
-    plans = [pipeline.sweep_plan(P, k, tour.xslot[:, g], chains=4) for g in range(P)]
-    pipeline.check_plan_coverage(plans, tour)
-    for pl in plans:
-        groups = pipeline.issue_groups(pl.items, True, max_group=4)
-        tasks = [g for g in groups if not isinstance(g, pipeline.Send)]
-        assert all(isinstance(g, tuple) and len(g) == 4 for g in tasks)
-        sends = [g for g in groups if isinstance(g, pipeline.Send)]
-        assert [s.half for s in sends] == [0, 1, 2, 3] * (2 * P - 2)
-
-
-def test_generalised_grouping_keeps_pairs():
-    """issue_groups with two chains groups exactly as the original pair rule."""
-    for P in (1, 2, 3, 4, 8):
-        tour = schedule.tournament(P)
-        for k in (2, 4, 6):
-            for g in range(P):
-                items = pipeline.sweep_plan(P, k, tour.xslot[:, g]).items
-                key = lambda x: tuple(map(id, x)) if isinstance(x, tuple) else id(x)  # noqa: E731
-                assert [key(x) for x in pipeline.issue_groups(items, True)] == \
-                    [key(x) for x in pipeline._issue_groups_pairs(items, True)]
-
-
 def test_dist_lib_resolves_to_shared_object():
     """ops._native.dist_lib() must load libsvdj_dist.so -- never the
     bin/svdj_dist_main launcher that build_dist() also produces (round-2
@@ -178,3 +149,13 @@ def test_dist_lib_resolves_to_shared_object():
     assert path == b.DIST_LIB and path.name == "libsvdj_dist.so"
     lib = nat.dist_lib()  # the exact loader bench.py --engine native uses
     assert hasattr(lib, "svdj_dist_solve") and hasattr(lib, "svdj_dist_comm_init")
+
+
+def test_chain_count_validated():
+    """Only the blocking (1) and pipelined two-chain (2) executors exist: any
+    other value is rejected when the config is built, not mid-solve."""
+    for bad in (0, 3, 4):
+        with pytest.raises(ValueError):
+            svdj.SolverConfig(chains=bad)
+    with pytest.raises(ValueError):
+        pipeline.sweep_plan(2, 4, schedule.tournament(2).xslot[:, 0], chains=4)

@@ -2,7 +2,6 @@
 # resident columns of m rows, kernel trace, per-stream gaps.
 # Usage: bash tools/gpu_latency_sim.sh NLOC M [extra bench args]
 set -o pipefail
-export SVDJ_NO_AUTOBUILD=1
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 NL=${1:-2048}; M=${2:-16384}; shift 2; EXTRA="$@"
 TAG=lat_${NL}_${M}${TAGX:-}

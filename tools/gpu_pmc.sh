@@ -5,7 +5,6 @@
 #   PMC_CMD="python3 tools/evd_ab.py --n 4096" overrides the profiled program
 #   PMC_PASSES="1 2" selects passes (default: all)
 set -o pipefail
-export SVDJ_NO_AUTOBUILD=1
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-pmc}; N=${2:-4096}; shift 2; EXTRA="$@"
 mkdir -p $OUT

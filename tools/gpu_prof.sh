@@ -1,7 +1,6 @@
 # Kernel-time profile of one bench solve per matrix-core mode (dev aid).
 # Usage: bash tools/gpu_prof.sh N "native bf16x6" [extra bench args]
 set -o pipefail
-export SVDJ_NO_AUTOBUILD=1
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=${1:-16384}; MODES=${2:-"native bf16x6"}; shift 2; EXTRA="$@"
 mkdir -p $R/gpurun_out
