@@ -44,41 +44,65 @@ BASELINE_METRIC = ("GFLOP/s + time-to-converge (sweeps to ||off||<tol), N×N den
                    "1/2/4/8 MI355X")
 
 
-def verify_distributed(res, gen, m, n, comm, dtype):
-    """Accuracy of the (distributed) result, after the timed region.
-
-    Every rank regenerates A (same seeded generator) and checks its own
-    columns: ||A V_loc - U_loc S_loc||_F^2 and ||[U_loc|V_loc]^T[..] - I||_F^2,
-    summed over ranks (fp32 GEMMs, accurate to ~1e-6 relative).  Padding
-    columns (global index >= n) are excluded."""
-    geo = res.info["geometry"]
-    B = geo["B"]
-    held = res.info["held"]
-    A = torch.cat([gen(c0, min(c0 + B, n)) for c0 in range(0, n, B)], dim=1).to(dtype)
-    At, Vt, S = res.U, res.V, res.S
-    cols = []
-    for s, sb in enumerate(held):
+def _global_columns(res, n, comm):
+    """Indices (rows of At / Vt / S) of this rank's real columns and their
+    global column ids, in slot order (padding columns >= n dropped)."""
+    B = res.info["geometry"]["B"]
+    loc, glob = [], []
+    for s_, sb in enumerate(res.info["held"]):
         for j in range(B):
             if sb * B + j < n:
-                cols.append(s * B + j)
-    idx = torch.tensor(cols, device=At.device, dtype=torch.long)
-    U = At[idx, :m].t()
-    V = Vt[idx, :n].t()
-    sig = S[idx]
+                loc.append(s_ * B + j)
+                glob.append(sb * B + j)
+    return loc, glob
+
+
+def verify_distributed(res, gen, m, n, comm, dtype):
+    """Accuracy of the distributed result, after the timed region.
+
+    Every rank regenerates A (same seeded generator) and checks its own
+    columns: ||A V_loc - U_loc S_loc||_F^2.  Orthogonality is FULL: U and V
+    are all-gathered in global column order and each rank forms its row
+    block U_loc^T U (V_loc^T V) of the n x n Gram, minus the identity;
+    the squared norms are summed over ranks (fp32 GEMMs, ~1e-6 relative)."""
+    loc, glob = _global_columns(res, n, comm)
+    A = gen(0, n).to(dtype)
+    dev = A.device
+    idx = torch.tensor(loc, device=res.U.device, dtype=torch.long)
+    U = res.U[idx, :m].t().to(dev)
+    V = res.V[idx, :n].t().to(dev)
+    sig = res.S[idx].to(dev)
     R = A @ V - U * sig
-    eye = torch.eye(len(cols), device=At.device, dtype=dtype)
+    gidx = torch.tensor(glob, device=dev, dtype=torch.long)
+    # all-gather (global id, column) of every rank's U and V columns
+    cnt = comm.allgather(torch.tensor([len(glob)], dtype=torch.int64, device=dev)).cpu().reshape(-1)
+    mx = int(cnt.max())
+    pad_u = torch.zeros(mx, m, dtype=dtype, device=dev)
+    pad_v = torch.zeros(mx, n, dtype=dtype, device=dev)
+    pad_g = torch.full((mx,), -1, dtype=torch.int64, device=dev)
+    pad_u[:len(glob)], pad_v[:len(glob)], pad_g[:len(glob)] = U.t(), V.t(), gidx
+    Uall, Vall, Gall = comm.allgather(pad_u), comm.allgather(pad_v), comm.allgather(pad_g)
+    Ufull = torch.zeros(n, m, dtype=dtype, device=dev)
+    Vfull = torch.zeros(n, n, dtype=dtype, device=dev)
+    for h in range(comm.world):
+        c = int(cnt[h])
+        Ufull[Gall[h, :c]] = Uall[h, :c]
+        Vfull[Gall[h, :c]] = Vall[h, :c]
+    del Uall, Vall
+    eye_rows = torch.zeros(len(glob), n, dtype=dtype, device=dev)
+    eye_rows[torch.arange(len(glob), device=dev), gidx] = 1
     parts = torch.stack([R.double().pow(2).sum(), A.double().pow(2).sum() / comm.world,
-                         (V.t() @ V - eye).double().pow(2).sum(),
-                         (U.t() @ U - eye).double().pow(2).sum()])
-    if comm.distributed:
-        import torch.distributed as dist
-        if dist.get_backend() == "gloo":  # host process group (--engine native)
-            parts = parts.cpu()
-        dist.all_reduce(parts)
-    parts = parts.cpu()
+                         (V.t() @ Vfull.t() - eye_rows).double().pow(2).sum(),
+                         (U.t() @ Ufull.t() - eye_rows).double().pow(2).sum()])
+    parts = comm.allreduce_sum_(parts.to(comm_device(comm, dev))).cpu()
     return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
-            "orth_v_blockdiag_fro": float(parts[2].sqrt()),
-            "orth_u_blockdiag_fro": float(parts[3].sqrt())}
+            "orth_v_fro": float(parts[2].sqrt()), "orth_u_fro": float(parts[3].sqrt()),
+            "orth_scope": "full n x n Gram (all-gathered)"}
+
+
+def comm_device(comm, dev):
+    """Device of the tensors the communicator reduces (host for gloo)."""
+    return torch.device("cpu") if getattr(comm, "backend", "") == "gloo" else dev
 
 
 def verify_rows(res, gen, m, n, comm, dtype):
@@ -101,7 +125,7 @@ def verify_rows(res, gen, m, n, comm, dtype):
             "orth_v_fro": float((V.t() @ V - eye).double().norm())}
 
 
-def sigma_check(res, gen, m, n, comm):
+def sigma_check(res, gen, m, n, comm):  # noqa: C901
     """max |sigma - sigma_ref| / sigma_ref_max against an fp64 oracle
     (torch.linalg.svdvals of the regenerated A in fp64 on the device,
     rocSOLVER), after the timed region.  Every rank's sigma columns are
@@ -109,7 +133,7 @@ def sigma_check(res, gen, m, n, comm):
     if res.info.get("distributed_output") is True:
         B = res.info["geometry"]["B"]
         ids = comm.allgather(torch.tensor(res.info["held"], device=res.S.device)).cpu()
-        S_all = comm.allgather(res.S)
+        S_all = comm.allgather(res.S[:2 * B])
         sig = torch.zeros(2 * B * comm.world, dtype=torch.float64, device=res.S.device)
         for h in range(comm.world):
             for s_ in range(2):
@@ -214,12 +238,30 @@ def simulate(a, cfg, dtype, work):
 
 
 class _HostComm:
-    """world / distributed / rank of the gloo host group of --engine native."""
+    """The gloo host group of --engine native (verification only: the solve
+    itself talks RCCL from C++)."""
+
+    backend = "gloo"
 
     def __init__(self, rank, world):
         self.rank, self.world = rank, world
 
     distributed = property(lambda self: self.world > 1)
+
+    def allgather(self, t):
+        if self.world == 1:
+            return t.unsqueeze(0).clone()
+        import torch.distributed as dist
+        h = t.detach().cpu().contiguous()
+        out = [torch.empty_like(h) for _ in range(self.world)]
+        dist.all_gather(out, h)
+        return torch.stack(out).to(t.device)
+
+    def allreduce_sum_(self, t):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t)
+        return t
 
 
 def run_native(a, dtype, work):
@@ -292,9 +334,10 @@ def run_native(a, dtype, work):
     B, ncols, m_pad, n_v = (g.value for g in geo)
     held0 = (C.c_int32 * 2)()
     check(lib.svdj_dist_initial_held(world, rank, held0), "svdj_dist_initial_held")
-    At = torch.zeros(2 * B, m_pad, dtype=dtype, device=dev)
-    Vt = torch.zeros(2 * B, n_v, dtype=dtype, device=dev)
-    D = torch.empty(2 * B, dtype=dtype, device=dev)
+    ncs = lib.svdj_dist_storage_cols(world, B)  # 2B + B of receive spares when P > 1
+    At = torch.zeros(ncs, m_pad, dtype=dtype, device=dev)
+    Vt = torch.zeros(ncs, n_v, dtype=dtype, device=dev)
+    D = torch.zeros(ncs, dtype=dtype, device=dev)
     S = torch.empty(2 * B, dtype=dtype, device=dev)
     gen = make_generator(m, dev, work, dtype)
     hist = (C.c_double * a.max_sweeps)()
@@ -307,6 +350,15 @@ def run_native(a, dtype, work):
     p.inner_order = 1 if a.inner_order == "bipartite" else 0
     p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
     p.hist = C.cast(hist, C.POINTER(C.c_double))
+    p.stagger = 1 if a.stagger else 0
+    p.timeout_s = float(timeout)
+    p.comm_timing = 1 if a.comm_timing else 0
+    p.fault_rank, p.fault_sweep = -1, -1
+    if a.inject_fault:
+        p.fault_rank, p.fault_sweep = (int(x) for x in a.inject_fault.split(":"))
+    hnd = C.c_void_p()  # persistent: workspaces, pair lists, events allocated once
+    check(lib.svdj_dist_handle_create(C.byref(p), C.byref(hnd)), "svdj_dist_handle_create")
+    p.handle = hnd
 
     def one():  # input generation (this rank's columns), V = I, norms, sweeps, U / sigma
         with torch.cuda.stream(sa):
@@ -320,7 +372,12 @@ def run_native(a, dtype, work):
             K.col_norms2(At, m_pad, out=D)
         p.held[0], p.held[1] = held0[0], held0[1]
         say(f"solve (W={W}, B={B}, m_pad={m_pad}, n_v={n_v})")
-        check(lib.svdj_dist_solve(C.byref(p), C.c_void_p(S.data_ptr())), "svdj_dist_solve")
+        rc = lib.svdj_dist_solve(C.byref(p), C.c_void_p(S.data_ptr()))
+        if rc == -300:  # watchdog: a peer died or hung; the communicator is aborted
+            print(f"[bench native rank {rank}] {lib.svdj_dist_last_error().decode()}",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
+        check(rc, "svdj_dist_solve")
         return p.sweeps, bool(p.converged)
 
     for _ in range(a.warmup):
@@ -347,8 +404,13 @@ def run_native(a, dtype, work):
             pass
         res = _Res()
         res.U, res.V, res.S = At, Vt, S
-        res.info = {"geometry": {"B": B}, "held": [int(p.held[0]), int(p.held[1])]}
+        res.info = {"geometry": {"B": B}, "held": [int(p.held[0]), int(p.held[1])],
+                    "distributed_output": True}
         acc = verify_distributed(res, gen, m, n, comm, work)
+        if want_sigma(a, n):
+            err = sigma_check(res, gen, m, n, comm)
+            if rank == 0:
+                acc["sigma_max_rel_err_vs_fp64_oracle"] = err
     if rank == 0:
         ms = el / a.steps * 1e3
         line = {
@@ -362,18 +424,31 @@ def run_native(a, dtype, work):
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
                        "mma": "native", "precondition": "none", "chains": 2,
                        "inner_order": a.inner_order,
-                       "staggered": os.environ.get("SVDJ_DIST_STAGGER") == "1", "root_owned": False},
+                       "staggered": bool(a.stagger), "root_owned": False},
             "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
+            "comm": ({"comm_ms": round(p.comm_ms, 3), "exposed_comm_ms": round(p.exposed_comm_ms, 3)}
+                     if a.comm_timing else None),
+            "world": world, "rccl_ranks": world,
             "accuracy": acc,
         }
         print(json.dumps(line), flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 json.dump(line, f)
+    lib.svdj_dist_handle_destroy(hnd)
     lib.svdj_dist_comm_destroy(nccl)
     if world > 1:
         dist.destroy_process_group()
+
+
+def want_sigma(a, n) -> bool:
+    """sigma vs the fp64 oracle: by default whenever n <= 8192 (rocSOLVER
+    svdvals of the regenerated A in fp64, after timing); --check-sigma forces
+    it, --no-sigma-check skips it."""
+    if a.no_sigma_check:
+        return False
+    return bool(a.check_sigma) or n <= 8192
 
 
 def svdj_default_inner() -> str:
@@ -410,7 +485,13 @@ def main():
                    help="A on rank 0 before timing; scatter + gather of U,S,V timed")
     p.add_argument("--progress", action="store_true", help="one line per sweep on stderr")
     p.add_argument("--comm-timeout", type=float, default=None,
-                   help="process-group timeout in s (default SVDJ_COMM_TIMEOUT or 600)")
+                   help="communication timeout in s: a peer that stops answering ends the "
+                        "job non-zero after this long (default SVDJ_COMM_TIMEOUT or 300)")
+    p.add_argument("--comm-timing", action="store_true",
+                   help="bracket every exchange and task with timing events and report "
+                        "comm_ms / exposed_comm_ms (adds events; off for headline runs)")
+    p.add_argument("--inject-fault", default=None, metavar="RANK:SWEEP",
+                   help="failure-detection test: that rank exits abruptly after that sweep")
     p.add_argument("--simulate-P", type=int, default=0)
     p.add_argument("--simulate-rank", type=int, default=0)
     p.add_argument("--sim-sweeps", type=int, default=3)
@@ -423,7 +504,9 @@ def main():
     p.add_argument("--no-verify", action="store_true",
                    help="skip the post-timing accuracy check")
     p.add_argument("--check-sigma", action="store_true",
-                   help="also compare sigma with an fp64 oracle (svdvals), after timing")
+                   help="compare sigma with an fp64 oracle (svdvals) even when n > 8192")
+    p.add_argument("--no-sigma-check", action="store_true",
+                   help="skip the sigma check that runs by default for n <= 8192")
     a = p.parse_args()
 
     import svdj
@@ -435,7 +518,12 @@ def main():
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
                             stagger=bool(a.stagger), precondition=a.precondition,
                             inner_order=a.inner_order,
-                            progress=a.progress, comm_timing=a.gpus > 1)
+                            progress=a.progress, comm_timing=a.comm_timing)
+    if a.inject_fault:
+        r_, s_ = (int(x) for x in a.inject_fault.split(":"))
+        cfg.extra["fault_exit"] = (r_, s_)
+    if a.comm_timeout is None:
+        a.comm_timeout = float(os.environ.get("SVDJ_COMM_TIMEOUT", "300"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     if a.simulate_P:
@@ -452,6 +540,14 @@ def main():
     comm = Communicator(timeout_s=a.comm_timeout)
     solver = DistributedBlockJacobi(cfg, comm)
     dev = comm.device
+    from svdj.parallel.schedule import tournament
+    tour = tournament(comm.world)
+    partners = set(tour.send_to[:, comm.rank].tolist()) | set(tour.recv_from[:, comm.rank].tolist())
+    ready = comm.readiness(partners)
+    if comm.rank == 0 and comm.distributed:
+        print(f"[bench] world {ready['world']} over {ready.get('rccl_ranks')} RCCL ranks, devices "
+              f"{ready.get('devices')}, P2P to tournament partners {ready.get('p2p_partners')}",
+              file=sys.stderr, flush=True)
     n = a.n
     m = a.m or n
     gen = make_generator(m, dev, work, dtype)
@@ -494,8 +590,15 @@ def main():
             acc = verify_rows(last, gen, m, n, comm, work)
         else:
             acc = verify_distributed(last, gen, m, n, comm, work)
-    if a.check_sigma and last.info.get("precondition") != "qr":
-        err = sigma_check(last, gen, m, n, comm)
+    if not a.no_verify and want_sigma(a, n) and last.info.get("precondition") != "qr":
+        if a.root_owned:
+            err = None
+            if comm.rank == 0:
+                ref = torch.linalg.svdvals(A_root.double())
+                got = torch.sort(last.S.double(), descending=True).values
+                err = float((got - ref).abs().max() / ref[0])
+        else:
+            err = sigma_check(last, gen, m, n, comm)
         if comm.rank == 0:
             acc = dict(acc or {}, sigma_max_rel_err_vs_fp64_oracle=err)
     if comm.rank == 0:
@@ -533,6 +636,8 @@ def main():
             "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % h) for h in last.history[-3:]],
             "comm": last.info.get("comm"),
+            "world": ready.get("world"), "devices": ready.get("devices"),
+            "rccl_ranks": ready.get("rccl_ranks"), "p2p_partners": ready.get("p2p_partners"),
             "accuracy": acc,
         }
         print(json.dumps(line), flush=True)

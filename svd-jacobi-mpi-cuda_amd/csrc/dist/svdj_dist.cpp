@@ -23,12 +23,17 @@
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <chrono>
 #include <cstdint>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "svdj_cpu.h"
@@ -87,16 +92,6 @@ struct Task {
   std::vector<int32_t> modes;
 };
 
-int upload(Task& t, const std::vector<int32_t>& host, int steps, int npairs,
-           std::vector<int32_t> modes) {
-  t.steps = steps;
-  t.npairs = npairs;
-  t.modes = std::move(modes);
-  HIPC(hipMalloc((void**)&t.pairs, host.size() * sizeof(int32_t)));
-  HIPC(hipMemcpy(t.pairs, host.data(), host.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  return 0;
-}
-
 }  // namespace
 
 extern "C" const char* svdj_dist_last_error(void) { return g_err; }
@@ -113,9 +108,15 @@ extern "C" int svdj_dist_comm_init(int rank, int world, const char* id_path, dou
     fclose(f);
     if (rename(tmp.c_str(), path.c_str()) != 0) return fail(-1, "cannot publish %s", path.c_str());
   } else {
+    // A file left by a crashed earlier job on the same path would hand this
+    // rank a dead id: only a file written since shortly before this call
+    // counts (rank 0 publishes within seconds of the others reaching here).
+    const time_t not_before = time(nullptr) - 30;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
-      FILE* f = fopen(path.c_str(), "rb");
+      struct stat sb;
+      FILE* f = (stat(path.c_str(), &sb) == 0 && sb.st_mtime >= not_before)
+                    ? fopen(path.c_str(), "rb") : nullptr;
       if (f) {
         const size_t got = fread(&id, sizeof(id), 1, f);
         fclose(f);
@@ -276,239 +277,613 @@ extern "C" int svdj_dist_plan(int world, int rank, int32_t* out, int cap) {
   return (int)groups.size();
 }
 
-// Two chains of a group: issued independently (default) or offset by an EVD
-// (svdj_block_steps2, SVDJ_DIST_STAGGER=1) -- the Python executor's
-// SolverConfig.stagger; independent issue measured faster since the
-// bipartite EVD and the round-2 apply geometry (profiles/r2_stag2).
-static bool stagger_on() {
-  static const bool on = [] {
-    const char* e = getenv("SVDJ_DIST_STAGGER");
-    return e && e[0] == '1';
-  }();
-  return on;
+extern "C" int svdj_dist_storage_cols(int world, int B) { return (world > 1 ? 3 : 2) * B; }
+
+namespace {
+
+// ---- where the resident halves live (parallel/pipeline.py HalfLayout).
+// Half buffers of hB columns: loc[slot][half] holds (slot, half); spare[h] is
+// the free buffer the next exchange of a half h receives into.  Buffers
+// {h, 2+h, 4+h} always hold (slot 0, h), (slot 1, h), spare.
+struct Layout {
+  int loc[2][2] = {{0, 1}, {2, 3}};
+  int spare[2] = {4, 5};
+};
+
+// Moves (src buffer, dst buffer) that bring every half home to buffer
+// 2 slot + half, parking one half in the spare when two sit in each other's
+// home (same rule as HalfLayout.moves_to_canonical).
+std::vector<std::pair<int, int>> moves_to_canonical(Layout& L) {
+  std::vector<std::pair<int, int>> mv;
+  for (int h = 0; h < 2; ++h) {
+    int where[2] = {L.loc[0][h], L.loc[1][h]}, free_b = L.spare[h];
+    for (int it = 0; it < 4; ++it) {
+      int todo[2], nt = 0;
+      for (int s = 0; s < 2; ++s)
+        if (where[s] != 2 * s + h) todo[nt++] = s;
+      if (!nt) break;
+      int pick = todo[0];
+      for (int q = 0; q < nt; ++q)
+        if (2 * todo[q] + h == free_b) pick = todo[q];
+      mv.push_back({where[pick], free_b});
+      const int old = where[pick];
+      where[pick] = free_b;
+      free_b = old;
+    }
+    L.loc[0][h] = where[0];
+    L.loc[1][h] = where[1];
+    L.spare[h] = free_b;
+  }
+  return mv;
 }
 
-extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
-  const int P = p->world, g = p->rank, W = p->W, B = p->B;
-  const int k = B / W, hk = k / 2, hB = hk * W;
-  if (B % W || k < 2 || k % 2) return fail(-2, "B=%d must hold an even number of W=%d blocks", B, W);
-  if (p->stream_a == p->stream_b) return fail(-2, "two distinct streams needed");
-  const size_t es = p->dtype == 1 ? 8 : 4;
-  hipStream_t st[2] = {(hipStream_t)p->stream_a, (hipStream_t)p->stream_b};
-  hipStream_t sa = st[0];
-  ncclComm_t comm = (ncclComm_t)p->comm;
-  const ncclDataType_t nt = p->dtype == 1 ? ncclFloat64 : ncclFloat32;
-  Tour tour(P);
+// Interval measure of union(waits) minus union(busy) (pipeline.exposed_time).
+double exposed_time(std::vector<std::pair<double, double>> w, std::vector<std::pair<double, double>> b) {
+  auto merge = [](std::vector<std::pair<double, double>>& v) {
+    std::sort(v.begin(), v.end());
+    std::vector<std::pair<double, double>> o;
+    for (auto& x : v) {
+      if (x.second <= x.first) continue;
+      if (!o.empty() && x.first <= o.back().second)
+        o.back().second = std::max(o.back().second, x.second);
+      else
+        o.push_back(x);
+    }
+    v.swap(o);
+  };
+  merge(w);
+  merge(b);
+  double total = 0;
+  size_t j = 0;
+  for (auto& x : w) {
+    double t = x.first;
+    while (j < b.size() && b[j].second <= t) ++j;
+    size_t k = j;
+    while (t < x.second) {
+      if (k < b.size() && b[k].first <= t) {
+        t = std::max(t, b[k].second);
+        ++k;
+        continue;
+      }
+      const double nxt = k < b.size() ? std::min(b[k].first, x.second) : x.second;
+      total += nxt - t;
+      t = nxt;
+    }
+  }
+  return total;
+}
 
-  // ---- plans (local block ids: slot s holds blocks [s k, (s+1) k))
+// A chain template: host pairs in canonical local block ids (slot*k +
+// half*hk + j) and the two halves it touches; one device copy per placement
+// of those halves (buffers bA, bB), built when the handle is created.
+struct Template {
+  std::vector<int32_t> host;
+  int steps = 0, npairs = 0;
+  std::vector<int32_t> modes;
+  int hv[2] = {0, 0};                 // halves touched (slot*2 + half)
+  int32_t* dev[6][6] = {};            // [buffer of hv[0]][buffer of hv[1]] -> device pairs
+};
+
+// Fail-fast watchdog: a thread polls the RCCL async
+// error and the time since the last finished sweep.  On a fault it takes the
+// NCCL lock (the solve holds it around every group of RCCL calls, so the
+// communicator is never freed under an enqueue), sets `fired` and calls
+// ncclCommAbort, which releases RCCL kernels spinning on the dead peer so
+// the streams drain; the solve returns -300 at its next check.  If the lock
+// cannot be had for 5 s (an enqueue itself is stuck), the process exits 3.
+struct Watchdog {
+  std::atomic<bool> stop{false}, fired{false};
+  std::mutex mu;  // held by the solve around RCCL calls
+  std::atomic<long long> last_ns{0};
+  char why[256] = {0};
+  std::thread th;
+  static long long now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void progress() { last_ns = now_ns(); }
+  void start(ncclComm_t comm, double timeout_s, int rank) {
+    progress();
+    th = std::thread([this, comm, timeout_s, rank]() {
+      while (!stop.load()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        ncclResult_t ae = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(comm, &ae);
+        const double idle = (now_ns() - last_ns.load()) * 1e-9;
+        if (q != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress)) {
+          snprintf(why, sizeof(why), "rank %d: RCCL async error: %s", rank,
+                   ncclGetErrorString(q != ncclSuccess ? q : ae));
+        } else if (idle > timeout_s) {
+          snprintf(why, sizeof(why), "rank %d: no sweep finished for %.0f s (peer dead or hung)",
+                   rank, idle);
+        } else {
+          continue;
+        }
+        fprintf(stderr, "[svdj_dist watchdog] %s: aborting the communicator\n", why);
+        fflush(stderr);
+        const long long t_lock = now_ns();
+        while (!mu.try_lock()) {
+          if ((now_ns() - t_lock) * 1e-9 > 5.0) {
+            fprintf(stderr, "[svdj_dist watchdog] rank %d: RCCL call stuck, exiting\n", rank);
+            fflush(stderr);
+            _exit(3);
+          }
+          std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        }
+        fired = true;
+        (void)ncclCommAbort(comm);
+        mu.unlock();
+        return;
+      }
+    });
+  }
+  void join() {
+    stop = true;
+    if (th.joinable()) th.join();
+  }
+};
+
+}  // namespace
+
+struct svdj_dist_handle_t {
+  int rank, world, dtype, W, m_pad, n_v, B, k, hk, hB, has_v, timing;
+  ncclComm_t comm;
+  hipStream_t st[2], sc;
+  bool own_sc = false;
+  size_t es, wsb;
+  void* ws[2] = {nullptr, nullptr};
+  uint32_t* metric = nullptr;
+  int32_t* pairs_pool = nullptr;
+  Template rr[2], cross[2][2][2];
+  std::vector<Item> items;
+  std::vector<Group> groups;
+  // per item: end event (task) / arrival (send); timing: start (task) / issue
+  // (send), consumer-ready events (two per task); plus sweep start and join
+  std::vector<hipEvent_t> ev, ev_start, ev_ready;
+  hipEvent_t ev_t0 = nullptr, ev_join = nullptr;
+  Layout L;
+};
+
+namespace {
+
+int build_templates(svdj_dist_handle_t* h, int cross_mode) {
+  const int k = h->k, hk = h->hk;
   std::vector<int32_t> rr((size_t)(k - 1) * (k / 2) * 2);
   svdj_round_robin(k, rr.data());
-  Task rr_task[2], cross[2][2][2];  // cross[incoming slot][I half][S half]
-  const int cross_mode = p->inner_order ? 2 : 0;  // svdj_block_steps mode of a cross step
   std::vector<int32_t> rr_modes(k - 1, cross_mode);
   rr_modes[0] = 1;  // the first step of a sweep re-measures the diagonal (full Gram)
-  int rc = 0;
-  for (int s = 0; s < 2 && !rc; ++s) {
-    std::vector<int32_t> h = rr;
-    for (auto& v : h) v += s * k;
-    rc = upload(rr_task[s], h, k - 1, k / 2, rr_modes);
+  for (int s = 0; s < 2; ++s) {
+    Template& t = h->rr[s];
+    t.host = rr;
+    for (auto& v : t.host) v += s * k;
+    t.steps = k - 1;
+    t.npairs = k / 2;
+    t.modes = rr_modes;
+    t.hv[0] = 2 * s;
+    t.hv[1] = 2 * s + 1;
   }
   for (int inc = 0; inc < 2; ++inc)
     for (int ih = 0; ih < 2; ++ih)
-      for (int sh = 0; sh < 2 && !rc; ++sh) {
+      for (int sh = 0; sh < 2; ++sh) {
         const int stay = 1 - inc;
-        std::vector<int32_t> h((size_t)hk * hk * 2);
-        for (int t = 0; t < hk; ++t)
+        Template& t = h->cross[inc][ih][sh];
+        t.host.assign((size_t)hk * hk * 2, 0);
+        for (int q = 0; q < hk; ++q)
           for (int a = 0; a < hk; ++a) {
-            h[(t * hk + a) * 2] = inc * k + ih * hk + a;
-            h[(t * hk + a) * 2 + 1] = stay * k + sh * hk + (a + t) % hk;
+            t.host[(q * hk + a) * 2] = inc * k + ih * hk + a;
+            t.host[(q * hk + a) * 2 + 1] = stay * k + sh * hk + (a + q) % hk;
           }
-        rc = upload(cross[inc][ih][sh], h, hk, hk, std::vector<int32_t>(hk, cross_mode));
+        t.steps = hk;
+        t.npairs = hk;
+        t.modes.assign(hk, cross_mode);
+        t.hv[0] = inc * 2 + ih;
+        t.hv[1] = stay * 2 + sh;
       }
-  const std::vector<Item> items = sweep_items(tour, g, rr_task, cross);
-  const std::vector<Group> groups = issue_groups(items);
+  // every placement of each template's two halves: half h lives in one of
+  // buffers {h, 2+h, 4+h} (only the canonical ones on one GPU)
+  std::vector<Template*> all = {&h->rr[0], &h->rr[1]};
+  for (auto& a : h->cross)
+    for (auto& b : a)
+      for (auto& c : b) all.push_back(&c);
+  const int nopt = h->world > 1 ? 3 : 1;
+  std::vector<int32_t> pool;
+  std::vector<std::tuple<Template*, int, int, size_t>> where;
+  for (Template* t : all)
+    for (int ia = 0; ia < nopt; ++ia)
+      for (int ib = 0; ib < nopt; ++ib) {
+        const int ha = t->hv[0] % 2, hb = t->hv[1] % 2;
+        const int ba = (ia == 0 ? t->hv[0] : (ia == 1 ? 2 * (1 - t->hv[0] / 2) + ha : 4 + ha));
+        const int bb = (ib == 0 ? t->hv[1] : (ib == 1 ? 2 * (1 - t->hv[1] / 2) + hb : 4 + hb));
+        if (ba == bb) continue;
+        where.emplace_back(t, ba, bb, pool.size());
+        for (int32_t v : t->host) {
+          const int slot = v / k, rem = v % k, half = rem / hk, off = rem % hk;
+          const int hvv = slot * 2 + half;
+          const int buf = hvv == t->hv[0] ? ba : bb;
+          pool.push_back(buf * hk + off);
+        }
+      }
+  HIPC(hipMalloc((void**)&h->pairs_pool, pool.size() * sizeof(int32_t)));
+  HIPC(hipMemcpy(h->pairs_pool, pool.data(), pool.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  for (auto& w : where) std::get<0>(w)->dev[std::get<1>(w)][std::get<2>(w)] = h->pairs_pool + std::get<3>(w);
+  return 0;
+}
 
-  // ---- workspaces (one per chain), metric, per-half receive buffers, events
-  const size_t wsb = svdj_block_workspace_bytes(p->dtype, W, k / 2, p->m_pad);
-  void* ws[2] = {nullptr, nullptr};
-  void *rA[2] = {nullptr, nullptr}, *rV[2] = {nullptr, nullptr}, *rD[2] = {nullptr, nullptr};
-  uint32_t* metric = nullptr;
-  hipStream_t sc = (hipStream_t)p->stream_comm;
-  const bool own_sc = sc == nullptr && P > 1;
-  std::vector<hipEvent_t> ev(items.size() + 4, nullptr);  // per item + ready, join, copied[2]
-  auto alloc = [&](void** q, size_t bytes) {
-    if (!rc && hipMalloc(q, bytes) != hipSuccess) rc = fail(-100, "hipMalloc(%zu) failed", bytes);
+void handle_free(svdj_dist_handle_t* h) {
+  if (!h) return;
+  for (auto* v : {&h->ev, &h->ev_start, &h->ev_ready})
+    for (auto& e : *v)
+      if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {h->ev_t0, h->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  if (h->own_sc && h->sc) (void)hipStreamDestroy(h->sc);
+  (void)hipFree(h->pairs_pool);
+  (void)hipFree(h->ws[0]);
+  (void)hipFree(h->ws[1]);
+  (void)hipFree(h->metric);
+  delete h;
+}
+
+}  // namespace
+
+extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
+  *out = nullptr;
+  const int W = p->W, B = p->B;
+  if (W <= 0 || B % W || (B / W) < 2 || (B / W) % 2)
+    return fail(-2, "B=%d must hold an even number of W=%d blocks", B, W);
+  if (p->stream_a == p->stream_b) return fail(-2, "two distinct streams needed");
+  auto* h = new svdj_dist_handle_t();
+  h->rank = p->rank, h->world = p->world, h->dtype = p->dtype, h->W = W, h->m_pad = p->m_pad;
+  h->n_v = p->n_v, h->B = B, h->k = B / W, h->hk = h->k / 2, h->hB = h->hk * W;
+  h->has_v = p->Vt != nullptr, h->timing = p->comm_timing != 0;
+  h->comm = (ncclComm_t)p->comm;
+  h->st[0] = (hipStream_t)p->stream_a;
+  h->st[1] = (hipStream_t)p->stream_b;
+  h->sc = (hipStream_t)p->stream_comm;
+  h->es = p->dtype == 1 ? 8 : 4;
+  int rc = 0;
+  auto guard = [&](int r) {
+    if (r < 0 && !rc) rc = r;
   };
-  for (int c = 0; c < 2; ++c) alloc(&ws[c], wsb);
-  alloc((void**)&metric, 2 * sizeof(uint32_t));
-  if (P > 1)
-    for (int h = 0; h < 2; ++h) {
-      alloc(&rA[h], (size_t)hB * p->m_pad * es);
-      alloc(&rD[h], (size_t)hB * es);
-      if (p->Vt) alloc(&rV[h], (size_t)hB * p->n_v * es);
+  guard(build_templates(h, p->inner_order ? 2 : 0));
+  h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
+  for (int c = 0; c < 2 && !rc; ++c)
+    if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);
+  if (!rc && hipMalloc((void**)&h->metric, 2 * sizeof(uint32_t)) != hipSuccess)
+    rc = fail(-100, "hipMalloc(metric) failed");
+  if (!rc && !h->sc && h->world > 1) {
+    if (hipStreamCreateWithFlags(&h->sc, hipStreamNonBlocking) != hipSuccess)
+      rc = fail(-100, "comm stream creation failed");
+    else
+      h->own_sc = true;
+  }
+  if (rc) {
+    handle_free(h);
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+
+extern "C" int svdj_dist_handle_destroy(void* handle) {
+  handle_free((svdj_dist_handle_t*)handle);
+  return 0;
+}
+
+namespace {
+
+// The issue plan of one rank on templates (same items / groups as
+// sweep_items / issue_groups, which tests compare with the Python plan).
+struct TItem {
+  bool send = false;
+  Template* t = nullptr;
+  int stream = 0;
+  int round = 0, slot = 0, half = 0;
+};
+
+std::vector<TItem> template_items(const Tour& tour, int g, svdj_dist_handle_t* h,
+                                  const std::vector<Item>& items) {
+  // sweep_items was built on dummy Tasks at fixed addresses: map them back
+  std::vector<TItem> out;
+  out.reserve(items.size());
+  for (const Item& x : items) {
+    TItem y;
+    y.send = x.send;
+    y.stream = x.stream;
+    y.round = x.round, y.slot = x.slot, y.half = x.half;
+    if (!x.send) {
+      // decode the halves: rr tasks touch (s,0),(s,1); cross (inc,ih),(stay,sh)
+      const int a = x.hv[0], b = x.hv[1];
+      if (a / 2 == b / 2) {
+        y.t = &h->rr[a / 2];
+      } else {
+        y.t = &h->cross[a / 2][a % 2][b % 2];
+      }
     }
-  if (!rc && own_sc && hipStreamCreateWithFlags(&sc, hipStreamNonBlocking) != hipSuccess)
-    rc = fail(-100, "comm stream creation failed");
-  for (auto& e : ev)
-    if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-      rc = fail(-100, "event creation failed");
-  hipEvent_t ev_ready = ev[items.size()], ev_join = ev[items.size() + 1];
-  hipEvent_t* ev_copied = &ev[items.size() + 2];
+    out.push_back(y);
+  }
+  (void)tour;
+  (void)g;
+  return out;
+}
+
+}  // namespace
+
+extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
+  svdj_dist_handle_t* h = (svdj_dist_handle_t*)p->handle;
+  bool own = false;
+  if (!h) {
+    void* hh = nullptr;
+    if (int r = svdj_dist_handle_create(p, &hh)) return r;
+    h = (svdj_dist_handle_t*)hh;
+    own = true;
+  }
+  struct Own {
+    svdj_dist_handle_t* h;
+    bool own;
+    ~Own() {
+      if (own) handle_free(h);
+    }
+  } own_guard{h, own};
+  if (h->rank != p->rank || h->world != p->world || h->dtype != p->dtype || h->W != p->W ||
+      h->m_pad != p->m_pad || h->n_v != p->n_v || h->B != p->B || h->has_v != (p->Vt != nullptr) ||
+      h->comm != (ncclComm_t)p->comm)
+    return fail(-2, "handle does not match the problem geometry");
+  const int P = h->world, g = h->rank, W = h->W, B = h->B, hB = h->hB;
+  const size_t es = h->es;
+  hipStream_t* st = h->st;
+  hipStream_t sa = st[0], sc = h->sc;
+  ncclComm_t comm = h->comm;
+  const ncclDataType_t nt = h->dtype == 1 ? ncclFloat64 : ncclFloat32;
+  Tour tour(P);
+
+  // issue plan (cached in the handle after the first solve)
+  if (h->items.empty()) {
+    Task rr_d[2], cross_d[2][2][2];
+    h->items = sweep_items(tour, g, rr_d, cross_d);
+    h->groups = issue_groups(h->items);
+    const unsigned flags = h->timing ? 0 : hipEventDisableTiming;
+    h->ev.assign(h->items.size(), nullptr);
+    for (auto& e : h->ev) HIPC(hipEventCreateWithFlags(&e, flags));
+    if (h->timing) {
+      h->ev_start.assign(h->items.size(), nullptr);
+      h->ev_ready.assign(2 * h->items.size(), nullptr);
+      for (auto* v : {&h->ev_start, &h->ev_ready})
+        for (auto& e : *v) HIPC(hipEventCreateWithFlags(&e, 0));
+      HIPC(hipEventCreateWithFlags(&h->ev_t0, 0));
+    }
+    HIPC(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  }
+  const std::vector<TItem> titems = template_items(tour, g, h, h->items);
+  const std::vector<Item>& items = h->items;
+  const std::vector<Group>& groups = h->groups;
+  Layout& L = h->L;
+  L = Layout();
+  if (P == 1) L.spare[0] = L.spare[1] = -1;
 
   // placement of every GPU's slots (all ranks simulate the whole table)
   std::vector<int32_t> phys(2 * P);
-  for (int h = 0; h < P; ++h) {
-    phys[2 * h] = tour.h(0, h, 0);
-    phys[2 * h + 1] = tour.h(0, h, 1);
+  for (int r = 0; r < P; ++r) {
+    phys[2 * r] = tour.h(0, r, 0);
+    phys[2 * r + 1] = tour.h(0, r, 1);
   }
-  if (!rc && (p->held[0] != phys[2 * g] || p->held[1] != phys[2 * g + 1]))
-    rc = fail(-2, "rank %d holds (%d, %d), the tournament starts from (%d, %d)", g, p->held[0],
-              p->held[1], phys[2 * g], phys[2 * g + 1]);
+  if (p->held[0] != phys[2 * g] || p->held[1] != phys[2 * g + 1])
+    return fail(-2, "rank %d holds (%d, %d), the tournament starts from (%d, %d)", g, p->held[0],
+                p->held[1], phys[2 * g], phys[2 * g + 1]);
 
-  auto rows = [&](int slot, int half) { return (size_t)slot * B + (size_t)half * hB; };
+  Watchdog wd;
+  const double timeout = p->timeout_s > 0 ? p->timeout_s : 600.0;
+  if (P > 1) wd.start(comm, timeout, g);
+  // Wait for stream sa without blocking forever: poll, and give up when the
+  // watchdog fired (a dead peer leaves RCCL kernels spinning; the abort
+  // releases them and the stream drains).
+  auto wait_sa = [&]() -> int {
+    for (;;) {
+      const hipError_t q = hipStreamQuery(sa);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady) return fail(-100, "stream error: %s", hipGetErrorString(q));
+      if (wd.fired.load()) return fail(-300, "%s", wd.why);
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  };
+  auto buf_ptr = [&](void* base, size_t ld, int b) { return (char*)base + (size_t)b * hB * ld * es; };
+  std::vector<std::pair<double, double>> busy, waits;
+  double comm_ms = 0, sweep_base_ms = 0;
   // One sweep: every dependency is an event; the host never waits.
   auto sweep = [&]() -> int {
     std::vector<hipEvent_t> last[4];   // task events on each half since its last exchange
-    hipEvent_t pending[4] = {nullptr, nullptr, nullptr, nullptr};  // arrived, not copied in
-    bool copied_used[2] = {false, false};
+    hipEvent_t pending[4] = {nullptr, nullptr, nullptr, nullptr};  // arrived, not yet waited
     int halves_sent = 0;
-    HIPC(hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), sa));
-    HIPC(hipEventRecord(ev_ready, sa));
-    HIPC(hipStreamWaitEvent(st[1], ev_ready, 0));
-    if (sc) HIPC(hipStreamWaitEvent(sc, ev_ready, 0));
-    auto consume = [&](int hv, hipStream_t s) -> int {
-      if (!pending[hv]) return 0;
-      HIPC(hipStreamWaitEvent(s, pending[hv], 0));
-      pending[hv] = nullptr;
-      const int slot = hv / 2, half = hv % 2;
-      const size_t r0 = rows(slot, half);
-      HIPC(hipMemcpyAsync((char*)p->At + r0 * p->m_pad * es, rA[half], (size_t)hB * p->m_pad * es,
-                          hipMemcpyDeviceToDevice, s));
-      HIPC(hipMemcpyAsync((char*)p->D + r0 * es, rD[half], (size_t)hB * es, hipMemcpyDeviceToDevice, s));
-      if (p->Vt)
-        HIPC(hipMemcpyAsync((char*)p->Vt + r0 * p->n_v * es, rV[half], (size_t)hB * p->n_v * es,
-                            hipMemcpyDeviceToDevice, s));
-      HIPC(hipEventRecord(ev_copied[half], s));  // the next receive into rV[half] waits on it
-      copied_used[half] = true;
-      return 0;
-    };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> sp_busy, sp_wait, sp_span;
+    HIPC(hipMemsetAsync(h->metric, 0, 2 * sizeof(uint32_t), sa));
+    if (h->timing) HIPC(hipEventRecord(h->ev_t0, sa));
+    HIPC(hipEventRecord(h->ev_join, sa));
+    HIPC(hipStreamWaitEvent(st[1], h->ev_join, 0));
+    if (sc) HIPC(hipStreamWaitEvent(sc, h->ev_join, 0));
     for (const Group& gr : groups) {
       const Item& a = items[gr.a];
       if (a.send) {  // one half of slot a.slot to send_to, its replacement from recv_from
         const int key = a.slot * 2 + a.half, dst = tour.to(a.round, g), src = tour.from(a.round, g);
+        const int out_b = L.loc[a.slot][a.half], in_b = L.spare[a.half];
         for (hipEvent_t e : last[key]) HIPC(hipStreamWaitEvent(sc, e, 0));
         last[key].clear();
-        if (copied_used[a.half]) HIPC(hipStreamWaitEvent(sc, ev_copied[a.half], 0));
-        const size_t r0 = rows(a.slot, a.half);
+        if (h->timing) HIPC(hipEventRecord(h->ev_start[gr.a], sc));
+        std::unique_lock<std::mutex> lk(wd.mu);
+        if (wd.fired.load()) return fail(-300, "%s", wd.why);
         NCCLC(ncclGroupStart());
-        NCCLC(ncclSend((char*)p->At + r0 * p->m_pad * es, (size_t)hB * p->m_pad, nt, dst, comm, sc));
-        NCCLC(ncclSend((char*)p->D + r0 * es, (size_t)hB, nt, dst, comm, sc));
-        NCCLC(ncclRecv(rA[a.half], (size_t)hB * p->m_pad, nt, src, comm, sc));
-        NCCLC(ncclRecv(rD[a.half], (size_t)hB, nt, src, comm, sc));
+        NCCLC(ncclSend(buf_ptr(p->At, h->m_pad, out_b), (size_t)hB * h->m_pad, nt, dst, comm, sc));
+        NCCLC(ncclSend((char*)p->D + (size_t)out_b * hB * es, (size_t)hB, nt, dst, comm, sc));
+        NCCLC(ncclRecv(buf_ptr(p->At, h->m_pad, in_b), (size_t)hB * h->m_pad, nt, src, comm, sc));
+        NCCLC(ncclRecv((char*)p->D + (size_t)in_b * hB * es, (size_t)hB, nt, src, comm, sc));
         if (p->Vt) {
-          NCCLC(ncclSend((char*)p->Vt + r0 * p->n_v * es, (size_t)hB * p->n_v, nt, dst, comm, sc));
-          NCCLC(ncclRecv(rV[a.half], (size_t)hB * p->n_v, nt, src, comm, sc));
+          NCCLC(ncclSend(buf_ptr(p->Vt, h->n_v, out_b), (size_t)hB * h->n_v, nt, dst, comm, sc));
+          NCCLC(ncclRecv(buf_ptr(p->Vt, h->n_v, in_b), (size_t)hB * h->n_v, nt, src, comm, sc));
         }
         NCCLC(ncclGroupEnd());
-        hipEvent_t arrived = ev[gr.a];
+        lk.unlock();
+        // received in place: from here on (issue order) the half lives in in_b;
+        // in_b's last readers were waited for by the exchange that freed it
+        L.loc[a.slot][a.half] = in_b;
+        L.spare[a.half] = out_b;
+        hipEvent_t arrived = h->ev[gr.a];
         HIPC(hipEventRecord(arrived, sc));
+        if (h->timing) sp_span.push_back({h->ev_start[gr.a], arrived});
         pending[key] = arrived;
         if (++halves_sent % 2 == 0) {  // both halves of round a.round issued: new placement
           std::vector<int32_t> old = phys;
-          for (int h = 0; h < P; ++h) {
-            const int sh = tour.from(a.round, h);
-            phys[2 * h + tour.x(a.round, h)] = old[2 * sh + tour.x(a.round, sh)];
+          for (int r = 0; r < P; ++r) {
+            const int sh = tour.from(a.round, r);
+            phys[2 * r + tour.x(a.round, r)] = old[2 * sh + tour.x(a.round, sh)];
           }
         }
         continue;
       }
       const int n_t = gr.b < 0 ? 1 : 2;
-      const Item* t[2] = {&a, gr.b < 0 ? nullptr : &items[gr.b]};
+      const int idx[2] = {gr.a, gr.b};
       for (int q = 0; q < n_t; ++q) {
-        hipStream_t s = st[t[q]->stream];
-        for (int hv : t[q]->hv) {
+        const Item& x = items[idx[q]];
+        hipStream_t s = st[x.stream];
+        int nready = 0;
+        for (int hv : x.hv) {
           for (hipEvent_t e : last[hv]) HIPC(hipStreamWaitEvent(s, e, 0));
-          if (int r2 = consume(hv, s)) return r2;
+          if (pending[hv]) {
+            if (h->timing) {
+              hipEvent_t r = h->ev_ready[2 * idx[q] + nready++];
+              HIPC(hipEventRecord(r, s));
+              sp_wait.push_back({r, pending[hv]});
+            }
+            HIPC(hipStreamWaitEvent(s, pending[hv], 0));
+            pending[hv] = nullptr;
+          }
         }
+        if (h->timing) HIPC(hipEventRecord(h->ev_start[idx[q]], s));
       }
-      const Task &x = *t[0]->task;
-      if (n_t == 2 && stagger_on()) {
-        const Task& y = *t[1]->task;
-        const int cx = t[0]->stream, cy = t[1]->stream;
-        SVDJC(svdj_block_steps2(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
-                                x.pairs, x.npairs, x.steps, x.modes.data(), ws[cx], wsb, st[cx],
-                                y.pairs, y.npairs, y.steps, y.modes.data(), ws[cy], wsb, st[cy],
-                                p->tol, p->tol_mode, 1, metric, p->mma));
+      auto dev_pairs = [&](const TItem& ti) {
+        const Template& t = *ti.t;
+        const int ba = L.loc[t.hv[0] / 2][t.hv[0] % 2], bb = L.loc[t.hv[1] / 2][t.hv[1] % 2];
+        return t.dev[ba][bb];
+      };
+      if (n_t == 2 && p->stagger) {
+        const TItem &x = titems[gr.a], &y = titems[gr.b];
+        const int cx = x.stream, cy = y.stream;
+        SVDJC(svdj_block_steps2(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
+                                dev_pairs(x), x.t->npairs, x.t->steps, x.t->modes.data(), h->ws[cx],
+                                h->wsb, st[cx], dev_pairs(y), y.t->npairs, y.t->steps,
+                                y.t->modes.data(), h->ws[cy], h->wsb, st[cy], p->tol, p->tol_mode,
+                                1, h->metric, p->mma));
       } else {
         for (int q = 0; q < n_t; ++q) {  // one chain, or two issued independently
-          const Task& z = *t[q]->task;
-          const int cz = t[q]->stream;
-          SVDJC(svdj_block_steps(p->dtype, W, p->m_pad, p->At, p->m_pad, p->Vt, p->n_v, p->n_v, p->D,
-                                 z.pairs, z.npairs, z.steps, z.modes.data(), p->tol, p->tol_mode, 1,
-                                 ws[cz], wsb, metric, p->mma, st[cz]));
+          const TItem& z = titems[idx[q]];
+          const int cz = z.stream;
+          SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
+                                 dev_pairs(z), z.t->npairs, z.t->steps, z.t->modes.data(), p->tol,
+                                 p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, p->mma, st[cz]));
         }
       }
       for (int q = 0; q < n_t; ++q) {
-        hipEvent_t e = ev[q == 0 ? gr.a : gr.b];
-        HIPC(hipEventRecord(e, st[t[q]->stream]));
-        for (int hv : t[q]->hv) last[hv].push_back(e);
+        const Item& x = items[idx[q]];
+        hipEvent_t e = h->ev[idx[q]];
+        HIPC(hipEventRecord(e, st[x.stream]));
+        if (h->timing) sp_busy.push_back({h->ev_start[idx[q]], e});
+        for (int hv : x.hv) last[hv].push_back(e);
       }
     }
-    HIPC(hipEventRecord(ev_join, st[1]));
-    HIPC(hipStreamWaitEvent(sa, ev_join, 0));
+    HIPC(hipEventRecord(h->ev_join, st[1]));
+    HIPC(hipStreamWaitEvent(sa, h->ev_join, 0));
+    if (sc) {
+      HIPC(hipEventRecord(h->ev_join, sc));
+      HIPC(hipStreamWaitEvent(sa, h->ev_join, 0));
+    }
+    if (h->timing) {  // diagnostics: resolve this sweep's events now
+      if (int r = wait_sa()) return r;
+      auto t = [&](hipEvent_t e) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, h->ev_t0, e);
+        return (double)ms;
+      };
+      for (auto& x : sp_busy) busy.push_back({t(x.first) + sweep_base_ms, t(x.second) + sweep_base_ms});
+      for (auto& x : sp_wait) waits.push_back({t(x.first) + sweep_base_ms, t(x.second) + sweep_base_ms});
+      for (auto& x : sp_span) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, x.first, x.second);
+        comm_ms += ms;
+      }
+      sweep_base_ms += 1e7;  // sweeps never overlap: keep their intervals apart
+    }
     return 0;
   };
 
-  if (!rc) {
-    p->sweeps = 0;
-    p->converged = 0;
-  }
+  int rc = 0;
+  p->sweeps = 0;
+  p->converged = 0;
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;
     // ---- stop test: global max convergence value (positive floats order as
     // uint32) and total rotated pairs
     uint32_t hm[2] = {0, 0};
     auto reduce = [&]() -> int {
-      NCCLC(ncclAllReduce(metric, metric, 1, ncclUint32, ncclMax, comm, sa));
-      NCCLC(ncclAllReduce(metric + 1, metric + 1, 1, ncclUint32, ncclSum, comm, sa));
-      HIPC(hipMemcpyAsync(hm, metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
-      HIPC(hipStreamSynchronize(sa));
-      return 0;
+      {
+        std::lock_guard<std::mutex> lk(wd.mu);
+        if (wd.fired.load()) return fail(-300, "%s", wd.why);
+        NCCLC(ncclAllReduce(h->metric, h->metric, 1, ncclUint32, ncclMax, comm, sa));
+        NCCLC(ncclAllReduce(h->metric + 1, h->metric + 1, 1, ncclUint32, ncclSum, comm, sa));
+      }
+      HIPC(hipMemcpyAsync(hm, h->metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
+      return wait_sa();
     };
     if ((rc = reduce())) break;
+    if (wd.fired.load()) {
+      rc = fail(-300, "%s", wd.why);
+      break;
+    }
+    wd.progress();
     float mx;
     memcpy(&mx, &hm[0], sizeof(float));
     if (p->hist) p->hist[sw] = mx;
     p->sweeps = sw + 1;
+    if (p->fault_rank == g && p->fault_sweep == sw + 1) {
+      fprintf(stderr, "[svdj_dist] fault injection: rank %d exits after sweep %d\n", g, sw + 1);
+      fflush(stderr);
+      _exit(17);
+    }
     if (hm[1] == 0) {
       p->converged = 1;
       break;
     }
   }
   if (!rc) {
+    // halves back home (rows [sB, (s+1)B) = slot s), then U and sigma
+    for (auto& mv : moves_to_canonical(L)) {
+      const size_t src = (size_t)mv.first, dst = (size_t)mv.second;
+      rc = rc ? rc : (hipMemcpyAsync(buf_ptr(p->At, h->m_pad, dst), buf_ptr(p->At, h->m_pad, src),
+                                     (size_t)hB * h->m_pad * es, hipMemcpyDeviceToDevice, sa) != hipSuccess
+                          ? fail(-100, "canonicalise copy failed") : 0);
+      if (!rc && p->Vt &&
+          hipMemcpyAsync(buf_ptr(p->Vt, h->n_v, dst), buf_ptr(p->Vt, h->n_v, src),
+                         (size_t)hB * h->n_v * es, hipMemcpyDeviceToDevice, sa) != hipSuccess)
+        rc = fail(-100, "canonicalise copy failed");
+      if (!rc && hipMemcpyAsync((char*)p->D + dst * hB * es, (char*)p->D + src * hB * es, hB * es,
+                                hipMemcpyDeviceToDevice, sa) != hipSuccess)
+        rc = fail(-100, "canonicalise copy failed");
+    }
     p->held[0] = phys[2 * g];
     p->held[1] = phys[2 * g + 1];
-    if (sigma) {
-      const int r2 = svdj_finalize(p->dtype, p->At, p->m_pad, p->m_pad, 2 * B, sigma, 1, sa);
+    if (!rc && sigma) {
+      const int r2 = svdj_finalize(h->dtype, p->At, h->m_pad, h->m_pad, 2 * B, sigma, 1, sa);
       if (r2 < 0) rc = fail(r2, "finalize: %s", svdj_hip_last_error());
     }
-    if (!rc && hipStreamSynchronize(sa) != hipSuccess) rc = fail(-100, "final sync failed");
-  } else {
+    if (!rc) rc = wait_sa();
+  }
+  wd.join();
+  if (rc == -300 || wd.fired.load()) {
+    p->comm = nullptr;  // aborted: the caller must not destroy it
+    if (!rc) rc = fail(-300, "%s", wd.why);
+  } else if (rc) {
     (void)hipDeviceSynchronize();  // nothing of this call may still run on its buffers
   }
-  for (auto& e : ev)
-    if (e) (void)hipEventDestroy(e);
-  if (own_sc && sc) (void)hipStreamDestroy(sc);
-  for (auto* t : {&rr_task[0], &rr_task[1]}) (void)hipFree(t->pairs);
-  for (auto& a : cross)
-    for (auto& b : a)
-      for (auto& c : b) (void)hipFree(c.pairs);
-  for (int h = 0; h < 2; ++h) {
-    (void)hipFree(ws[h]);
-    (void)hipFree(rA[h]);
-    (void)hipFree(rD[h]);
-    (void)hipFree(rV[h]);
+  if (h->timing) {
+    p->comm_ms = comm_ms;
+    p->exposed_comm_ms = exposed_time(waits, busy);
   }
-  (void)hipFree(metric);
   return rc;
 }

@@ -7,7 +7,7 @@
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
 //                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
-//                  [--id-file PATH]
+//                  [--id-file PATH] [--comm-timing] [--inject-fault RANK:SWEEP] [--keep-going]
 //
 // The launcher forks P ranks before anything touches the GPU (the parent never
 // does) and waits for them; a rank that fails or a job that exceeds --timeout
@@ -19,16 +19,24 @@
 // Rank g selects GPU LOCAL_RANK (or g); --shared-gpu puts every rank on GPU 0
 // and gives each its own NCCL_HOSTID so RCCL accepts several ranks on one
 // device (transport: sockets on loopback, for rehearsal on a one-GPU box).
-// Every rank generates the reference input (svdj_ref_*_input) and keeps the
-// columns of the two super-blocks the tournament starts it with; rank 0
-// prints the reference's lines and, with --verify, gathers U, S, V and checks
-// ||A - U S V^T||_F and orthogonality in fp64 on the host.
+// Every rank draws the reference input stream (svdj_ref_input_cols) and
+// stores only the columns of the two super-blocks the tournament starts it
+// with; rank 0 prints the reference's lines and, with --verify, also keeps
+// the whole A, gathers U, S, V and checks ||A - U S V^T||_F and
+// orthogonality in fp64 on the host.
+//
+// Failure handling: every solve runs under the library's watchdog (an RCCL
+// async error, or no sweep finished within --timeout seconds, aborts the
+// communicator and the rank exits 3).  --inject-fault R:S makes rank R exit
+// abruptly after sweep S; with --keep-going the launcher does not stop the
+// other ranks on a failure, so the survivors' own detection is what ends them.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -46,9 +54,11 @@ namespace {
 
 struct Opts {
   int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 1;
+  int fault_rank = -1, fault_sweep = -1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
   bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;
+  bool comm_timing = false, keep_going = false;
   std::string id_file;
 };
 
@@ -99,27 +109,36 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   }
   int32_t held[2];
   svdj_dist_initial_held(world, rank, held);
+  const int ncs = svdj_dist_storage_cols(world, B);  // 2B (+ B of receive spares)
 
-  // reference input (every rank draws the same stream), keep this rank's columns
-  std::vector<double> A((size_t)m * n, 0.0);
-  if (o.dense)
-    svdj_ref_dense_input(m, n, A.data(), m, o.seed);
-  else
-    svdj_ref_triu_input(m, n, A.data(), m, o.seed);
+  // reference input: every rank draws the same stream and stores only its
+  // two super-blocks (rank 0 with --verify also the whole A)
+  std::vector<double> A;
+  if (rank == 0 && o.verify) {
+    A.assign((size_t)m * n, 0.0);
+    if (o.dense)
+      svdj_ref_dense_input(m, n, A.data(), m, o.seed);
+    else
+      svdj_ref_triu_input(m, n, A.data(), m, o.seed);
+  }
   std::vector<T> hA((size_t)2 * B * m_pad, T(0));
-  for (int s = 0; s < 2; ++s)
-    for (int c = 0; c < B; ++c) {
-      const int j = held[s] * B + c;
-      if (j >= n) break;
-      for (int i = 0; i < m; ++i) hA[(size_t)(s * B + c) * m_pad + i] = (T)A[(size_t)j * m + i];
+  {
+    std::vector<double> cols;
+    for (int s = 0; s < 2; ++s) {
+      const int c0 = held[s] * B, nc = std::min(B, n - c0);
+      if (nc <= 0) continue;
+      cols.assign((size_t)nc * m, 0.0);
+      svdj_ref_input_cols(m, n, o.dense ? 1 : 0, o.seed, c0, nc, cols.data(), m);
+      for (int c = 0; c < nc; ++c)
+        for (int i = 0; i < m; ++i) hA[(size_t)(s * B + c) * m_pad + i] = (T)cols[(size_t)c * m + i];
     }
-  if (rank != 0 || !o.verify) std::vector<double>().swap(A);
+  }
 
   T *dA, *dV = nullptr, *dD, *dS;
   double* dt;
-  CK(hipMalloc((void**)&dA, hA.size() * sizeof(T)));
-  if (o.want_v) CK(hipMalloc((void**)&dV, (size_t)2 * B * n_v * sizeof(T)));
-  CK(hipMalloc((void**)&dD, (size_t)2 * B * sizeof(T)));
+  CK(hipMalloc((void**)&dA, (size_t)ncs * m_pad * sizeof(T)));
+  if (o.want_v) CK(hipMalloc((void**)&dV, (size_t)ncs * n_v * sizeof(T)));
+  CK(hipMalloc((void**)&dD, (size_t)ncs * sizeof(T)));
   CK(hipMalloc((void**)&dS, (size_t)2 * B * sizeof(T)));
   CK(hipMalloc((void**)&dt, sizeof(double)));
   double tol = o.tol;
@@ -147,6 +166,15 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.stream_b = sb;
   p.stream_comm = sc;
   p.hist = hist.data();
+  p.timeout_s = o.timeout;
+  p.comm_timing = o.comm_timing ? 1 : 0;
+  p.fault_rank = o.fault_rank;
+  p.fault_sweep = o.fault_sweep;
+  // persistent handle: workspaces, pair lists and events once, not per solve
+  if (svdj_dist_handle_create(&p, &p.handle) < 0) {
+    std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
+    return 2;
+  }
   double secs = 0;
   // --warmup solves first (RCCL connects its peers lazily, on the first
   // send/recv), then the timed one; each starts from the original columns
@@ -167,9 +195,10 @@ int run_rank(const Opts& o, int rank, int world, int device) {
       std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_hip_last_error());
       return 2;
     }
-    if (svdj_dist_solve(&p, dS) < 0) {
+    if (const int r = svdj_dist_solve(&p, dS); r < 0) {
       std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
-      return 2;
+      std::fflush(stderr);
+      return r == -300 ? 3 : 2;  // -300: watchdog abort (the communicator is gone)
     }
     secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     CK(hipMemcpy(dt, &secs, sizeof(double), hipMemcpyHostToDevice));
@@ -188,6 +217,8 @@ int run_rank(const Opts& o, int rank, int world, int device) {
                 p.converged, p.sweeps > 0 ? hist[p.sweeps - 1] : 0.0, tol);
     const double flops = (double)n * (n - 1) / 2.0 * (12.0 * m + (o.want_v ? 6.0 * n : 0.0)) * p.sweeps;
     std::printf("GFLOP/s (algorithmic): %.1f\n", flops / secs / 1e9);
+    if (o.comm_timing)
+      std::printf("comm_ms: %.3f  exposed_comm_ms: %.3f\n", p.comm_ms, p.exposed_comm_ms);
   }
 
   int rc = 0;
@@ -281,6 +312,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   (void)hipFree(dD);
   (void)hipFree(dS);
   (void)hipFree(dt);
+  svdj_dist_handle_destroy(p.handle);
   svdj_dist_comm_destroy(comm);
   return rc;
 }
@@ -336,6 +368,18 @@ int main(int argc, char** argv) {
     else if (a == "--warmup") o.warmup = std::atoi(next());
     else if (a == "--inner") o.inner = std::string(next()) == "bipartite" ? 1 : 0;
     else if (a == "--id-file") o.id_file = next();
+    else if (a == "--comm-timing") o.comm_timing = true;
+    else if (a == "--keep-going") o.keep_going = true;
+    else if (a == "--inject-fault") {
+      const std::string v = next();
+      const size_t c = v.find(':');
+      if (c == std::string::npos) {
+        std::fprintf(stderr, "--inject-fault RANK:SWEEP\n");
+        return 1;
+      }
+      o.fault_rank = std::atoi(v.substr(0, c).c_str());
+      o.fault_sweep = std::atoi(v.substr(c + 1).c_str());
+    }
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());
       return 1;
@@ -354,7 +398,9 @@ int main(int argc, char** argv) {
     if (o.id_file.empty()) {
       const char* e = std::getenv("SVDJ_DIST_ID");
       const char* port = std::getenv("MASTER_PORT");
-      o.id_file = e ? e : std::string("/tmp/svdj_dist_") + (port ? port : "0") + ".id";
+      const char* run = std::getenv("TORCHELASTIC_RUN_ID");  // unique per torchrun job
+      o.id_file = e ? e : std::string("/tmp/svdj_dist_") + (port ? port : "0") +
+                              (run && std::strcmp(run, "none") ? std::string("_") + run : "") + ".id";
     }
     const char* lr = std::getenv("LOCAL_RANK");
     const int rank = std::atoi(env_rank);
@@ -404,7 +450,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "rank %d exited with %d; stopping the job\n", who, code);
         if (!worst) {
           worst = code;
-          stop_others(SIGTERM);
+          if (!o.keep_going) stop_others(SIGTERM);
         }
       }
       continue;

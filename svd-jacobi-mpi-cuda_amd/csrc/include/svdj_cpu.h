@@ -78,6 +78,9 @@ void svdj_ref_dense_input(int m, int n, double* A, int lda, uint32_t seed);
 // First `count` raw draws of uniform_real_distribution<double>(0,1) with
 // default_random_engine(seed) -- used by tests to pin bit parity.
 void svdj_ref_uniform_stream(uint32_t seed, int count, double* out);
+// Columns [c0, c0 + nc) of the triangular (dense = 0) / dense (dense = 1)
+// input into out (ld >= m), without storing the rest of the matrix.
+void svdj_ref_input_cols(int m, int n, int dense, uint32_t seed, int c0, int nc, double* out, int ld);
 
 // --------------------------------------------------------------- verification
 // ||A - U diag(s) V^T||_F for column-major inputs (blocked, OpenMP).

@@ -5,12 +5,14 @@
 // driven from main.cu:1587; lib/JacobiMethods.cuh:44-52).  This is the
 // MI355X-native equivalent without Python: the super-block tournament of
 // svdj_tournament (2P super-blocks, 2P-1 rounds, one super-block exchanged
-// per GPU per round), the block steps of libsvdj_hip on two staggered chains,
-// and an RCCL all-reduce of the sweep's convergence value and rotation count
-// as the stop test.  The exchange is pipelined as in parallel/pipeline.py:
-// each super-block moves in two halves with grouped ncclSend/ncclRecv on a
-// comm stream as soon as the tasks touching that half are done, and consumers
-// wait on the arrival event -- the host never blocks inside a sweep.
+// per GPU per round), the block steps of libsvdj_hip on two chains, and an
+// RCCL all-reduce of the sweep's convergence value and rotation count as the
+// stop test.  The exchange is pipelined as in parallel/pipeline.py: each
+// super-block moves in two halves with grouped ncclSend/ncclRecv on a comm
+// stream as soon as the tasks touching that half are done, received in place
+// into a spare half buffer, and consumers wait on the arrival event -- the
+// host never blocks inside a sweep.  A watchdog thread aborts the
+// communicator on an RCCL async error or when no sweep finishes in time.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -39,14 +41,21 @@ int svdj_dist_choose_block(int dtype, int world, int m, int n);
 // Super-block ids held by `rank` at the start of a sweep (round 0 placement).
 int svdj_dist_initial_held(int world, int rank, int32_t held[2]);
 
+// Rows of At / Vt / entries of D a rank allocates for super-blocks of B
+// columns: 2B on one GPU, 3B with exchanges -- the two extra half buffers
+// are the receive spares (exchanges receive in place, no copy-in).  Rows
+// [0, 2B) hold slot 0 | slot 1 before and after svdj_dist_solve.
+int svdj_dist_storage_cols(int world, int B);
+
 typedef struct {
   int rank, world;
   void* comm;                 // ncclComm_t (svdj_dist_comm_init)
   int dtype;                  // 0 fp32, 1 fp64
   int W, m_pad, n_v, B;       // from svdj_dist_geometry
-  void* At;                   // (2B, m_pad) transposed columns: slot s = rows [sB, (s+1)B)
-  void* Vt;                   // (2B, n_v) or NULL (no V)
-  void* D;                    // (2B) squared column norms (svdj_col_norms2)
+  void* At;                   // (svdj_dist_storage_cols, m_pad) transposed columns:
+                              // slot s = rows [sB, (s+1)B) on entry and on return
+  void* Vt;                   // (svdj_dist_storage_cols, n_v) or NULL (no V)
+  void* D;                    // (svdj_dist_storage_cols) squared column norms
   int32_t held[2];            // in: svdj_dist_initial_held (the data must be placed so);
                               // out: super-blocks in the two slots after the last sweep
   double tol;
@@ -54,20 +63,40 @@ typedef struct {
   int max_sweeps;
   int mma;                    // matrix-core mode of the apply (svdj_block_steps)
   int inner_order;            // EVD of the cross steps: 0 cyclic, 1 bipartite (mode 2)
+  int stagger;                // 1: the two chains of a group offset by an EVD
+                              // (svdj_block_steps2); 0 (default): issued independently
   void* stream_a;             // two compute streams (distinct)
   void* stream_b;
-  void* stream_comm;          // exchange stream, or NULL (created per call).  HIP maps
+  void* stream_comm;          // exchange stream, or NULL (created by the handle).  HIP maps
                               // streams onto GPU_MAX_HW_QUEUES hardware queues as they
                               // are created: make the three streams first, before RCCL's
                               // own, or two of them may share a queue and serialise.
+  double timeout_s;           // watchdog: no finished sweep for this long, or an RCCL
+                              // async error -> ncclCommAbort and return -300 (<= 0: 600 s)
+  int comm_timing;            // 1: timing events on every exchange and task
+  int fault_rank, fault_sweep;  // test hook: that rank _exit(17)s after that sweep (-1: off)
+  void* handle;               // svdj_dist_handle_create, or NULL (one per call)
   double* hist;               // host [max_sweeps]: per-sweep global max convergence value
   int sweeps;                 // out
   int converged;              // out
+  double comm_ms;             // out (comm_timing): sum of exchange spans
+  double exposed_comm_ms;     // out (comm_timing): time some compute stream waited for an
+                              // arrival while no task ran on either compute stream
 } svdj_dist_problem;
+
+// Persistent per-rank state for repeated solves of one geometry: workspaces,
+// metric, every device pair list of the plan (for each placement of the
+// halves), events and the comm stream -- allocated once, so a solve
+// allocates nothing.  Reads rank, world, comm, dtype, W, m_pad, n_v, B,
+// Vt (NULL or not), the streams and comm_timing from *p.
+int svdj_dist_handle_create(const svdj_dist_problem* p, void** handle);
+int svdj_dist_handle_destroy(void* handle);
 
 // Runs sweeps until one applies no rotation anywhere (or max_sweeps), then
 // normalises U in place (At rows) and writes sigma[2B] (device, data type).
-// Collective: every rank calls it.  Returns 0 or <0 (svdj_dist_last_error()).
+// Collective: every rank calls it.  Returns 0 or <0 (svdj_dist_last_error());
+// -300: the watchdog aborted the communicator (a peer died or hung) -- the
+// communicator is then unusable and must not be destroyed.
 int svdj_dist_solve(svdj_dist_problem* p, void* sigma);
 
 // Issue order of one sweep on `rank` (host only, for tests): per group 7 ints

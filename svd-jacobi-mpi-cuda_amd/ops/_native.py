@@ -139,9 +139,11 @@ class DistProblem(C.Structure):
                 ("W", c_int), ("m_pad", c_int), ("n_v", c_int), ("B", c_int),
                 ("At", c_void_p), ("Vt", c_void_p), ("D", c_void_p), ("held", C.c_int32 * 2),
                 ("tol", c_double), ("tol_mode", c_int), ("max_sweeps", c_int), ("mma", c_int),
-                ("inner_order", c_int), ("stream_a", c_void_p), ("stream_b", c_void_p),
-                ("stream_comm", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
-                ("converged", c_int)]
+                ("inner_order", c_int), ("stagger", c_int), ("stream_a", c_void_p),
+                ("stream_b", c_void_p), ("stream_comm", c_void_p), ("timeout_s", c_double),
+                ("comm_timing", c_int), ("fault_rank", c_int), ("fault_sweep", c_int),
+                ("handle", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
+                ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double)]
 
 
 def dist_lib_path() -> Path:
@@ -177,6 +179,9 @@ def dist_lib():
         _sig(lib, "svdj_dist_choose_block", c_int, [c_int, c_int, c_int, c_int])
         _sig(lib, "svdj_dist_initial_held", c_int, [c_int, c_int, c_i32_p])
         _sig(lib, "svdj_dist_solve", c_int, [C.POINTER(DistProblem), c_void_p])
+        _sig(lib, "svdj_dist_storage_cols", c_int, [c_int, c_int])
+        _sig(lib, "svdj_dist_handle_create", c_int, [C.POINTER(DistProblem), C.POINTER(c_void_p)])
+        _sig(lib, "svdj_dist_handle_destroy", c_int, [c_void_p])
         _sig(lib, "svdj_dist_last_error", C.c_char_p, [])
         _dist = lib
         return lib

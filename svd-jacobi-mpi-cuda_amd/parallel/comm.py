@@ -42,7 +42,8 @@ def env_world() -> tuple[int, int, int]:
 
 
 def default_timeout_s() -> float:
-    """Process-group timeout: ``SVDJ_COMM_TIMEOUT`` seconds (default 600).  A
+    """Process-group timeout: ``SVDJ_COMM_TIMEOUT`` seconds (default 600;
+    bench.py uses 300).  A
     collective or p2p op that does not finish in time makes the RCCL watchdog
     abort the process (TORCH_NCCL_ASYNC_ERROR_HANDLING), so a hung peer ends
     the job with a non-zero exit instead of hanging it."""
@@ -103,6 +104,48 @@ class Communicator:
         exchange is enqueued after the issuing stream's work and completion is
         a stream dependency, never a host wait."""
         return self.backend == "nccl" and self.device.type == "cuda"
+
+    # ------------------------------------------------------------ readiness
+    def readiness(self, partners=()) -> dict:
+        """Check and report the process -> GPU mapping of a multi-rank job.
+
+        Every rank contributes (host, device index, local device count); the
+        ranks must sit on distinct (host, device) pairs -- one process per
+        GPU -- unless SVDJ_SHARED_GPU=1 (one-GPU rehearsal).  ``partners``
+        (the tournament peers of this rank) are probed for peer access
+        (hipDeviceCanAccessPeer: xGMI P2P) when on the same host.  Raises
+        RuntimeError on a bad mapping, so a misconfigured 8-GPU launch fails
+        before any sweep instead of time-sharing a device."""
+        info = {"world": self.world, "backend": self.backend}
+        if self.device.type != "cuda":
+            return info
+        import socket
+        import zlib
+
+        host = zlib.crc32(socket.gethostname().encode()) & 0x7FFFFFFF
+        idx = self.device.index if self.device.index is not None else 0
+        peers = sorted({int(p) for p in partners if 0 <= int(p) < self.world and int(p) != self.rank})
+        me = torch.tensor([host, idx, torch.cuda.device_count(), len(peers), 0],
+                          dtype=torch.int64, device=self.device)
+        rows = self.allgather(me).cpu().tolist() if self.distributed else [me.tolist()]
+        shared = os.environ.get("SVDJ_SHARED_GPU") == "1"
+        pairs = {(r[0], r[1]) for r in rows}
+        if len(pairs) != len(rows) and not shared:
+            raise RuntimeError(f"ranks share a GPU (host, device) = "
+                               f"{[(r[0], r[1]) for r in rows]}: launch one process per GPU "
+                               "(device = cuda:LOCAL_RANK) or set SVDJ_SHARED_GPU=1")
+        ok = 0
+        for p in peers:
+            h, d = rows[p][0], rows[p][1]
+            if h == host and d != idx:
+                ok += int(torch.cuda.can_device_access_peer(idx, d))
+        me[4] = ok
+        rows = self.allgather(me).cpu().tolist() if self.distributed else [me.tolist()]
+        info.update(devices=[int(r[1]) for r in rows], hosts=len({r[0] for r in rows}),
+                    rccl_ranks=dist.get_world_size() if dist.is_initialized() else 1,
+                    shared_gpu=shared,
+                    p2p_partners=[f"{int(r[4])}/{int(r[3])}" for r in rows])
+        return info
 
     # ---------------------------------------------------------------- p2p
     def _ops(self, sends: list, recvs: list) -> list:

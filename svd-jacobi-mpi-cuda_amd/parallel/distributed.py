@@ -244,18 +244,25 @@ class DistributedBlockJacobi(Solver):
         # rank simulates the whole table (exchanges are deterministic).
         phys = [[int(tour.held[0, h, 0]), int(tour.held[0, h, 1])] for h in range(P)]
         held = phys[g]
-        At = torch.zeros(2 * B, m_pad, dtype=dtype, device=dev)
+        # pipelined multi-rank storage carries one spare half buffer per half
+        # index (the exchanges receive in place, pipeline.HalfLayout); rows
+        # [0, 2B) are the canonical slots at the start and after the solve
+        ncol_store = PipelineExecutor.storage_columns(B, comm.distributed) if pipelined else 2 * B
+        At = torch.zeros(ncol_store, m_pad, dtype=dtype, device=dev)
         want_v = jobv != SVDOptions.NoVec
-        Vt = torch.zeros(2 * B, n_v, dtype=dtype, device=dev) if want_v else None
+        Vt = torch.zeros(ncol_store, n_v, dtype=dtype, device=dev) if want_v else None
         self._distribute(A, generator, At, held, m, n, B, dtype)
         if want_v:
             for s in range(2):
                 K.set_identity(Vt[s * B:(s + 1) * B], B, held[s] * B)
         D = K.col_norms2(At, m_pad)
         tol = self.tolerance(pdtype, m)
-        rA = torch.empty(B, m_pad, dtype=dtype, device=dev)
-        rV = torch.empty(B, n_v, dtype=dtype, device=dev) if want_v else None
-        rD = torch.empty(B, dtype=dtype, device=dev)
+        if pipelined:
+            rA = rV = rD = None
+        else:  # blocking exchange (chains=1) receives into a staging block
+            rA = torch.empty(B, m_pad, dtype=dtype, device=dev)
+            rV = torch.empty(B, n_v, dtype=dtype, device=dev) if want_v else None
+            rD = torch.empty(B, dtype=dtype, device=dev)
         metric = K.new_metric(dev)
         comm.barrier()
 
@@ -267,10 +274,10 @@ class DistributedBlockJacobi(Solver):
         if cfg.checkpoint_dir:
             st = ckpt.load(cfg.checkpoint_dir, g, dev)
             if st is not None and ckpt.compatible(st, sig):
-                At.copy_(st["At"])
-                D.copy_(st["D"])
+                At[:2 * B].copy_(st["At"])
+                D[:2 * B].copy_(st["D"])
                 if want_v:
-                    Vt.copy_(st["Vt"])
+                    Vt[:2 * B].copy_(st["Vt"])
                 phys = [list(x) for x in st["phys"]]
                 held = phys[g]
                 hist = list(st["hist"])
@@ -326,11 +333,18 @@ class DistributedBlockJacobi(Solver):
             # placement: the schedule only depends on positions, so every
             # physical pair still meets exactly once per sweep.
             if cfg.checkpoint_dir and cfg.checkpoint_every and sweeps % cfg.checkpoint_every == 0:
+                if pipelined:
+                    ex.canonicalize()
                 ckpt.save(cfg.checkpoint_dir, g,
-                          {**sig, "At": At, "Vt": Vt if want_v else torch.empty(0), "D": D,
-                           "phys": phys, "hist": hist, "sweep": sweeps})
+                          {**sig, "At": At[:2 * B], "Vt": Vt[:2 * B] if want_v else torch.empty(0),
+                           "D": D[:2 * B], "phys": phys, "hist": hist, "sweep": sweeps})
+            self._fault_point(sweeps)
         if converged and cfg.checkpoint_dir:
             ckpt.clear(cfg.checkpoint_dir, g)
+        if pipelined:
+            ex.canonicalize()
+            At, D = At[:2 * B], D[:2 * B]
+            Vt = Vt[:2 * B] if want_v else None
         sigma_loc = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         sync()
         t_total = time.perf_counter() - t0
@@ -347,6 +361,17 @@ class DistributedBlockJacobi(Solver):
             U = U.to(torch.bfloat16) if U is not None else None
             V = V.to(torch.bfloat16) if V is not None else None
         return SVDResult(U, S, V, sweeps, hist, t_total, self.name, info)
+
+    def _fault_point(self, sweeps: int):
+        """Fault injection for failure-detection tests: SolverConfig.extra
+        ["fault_exit"] = (rank, sweep) makes that rank exit abruptly (no
+        cleanup, exit status 17) after that sweep, like a crashed peer."""
+        f = self.config.extra.get("fault_exit") if self.config.extra else None
+        if f and int(f[0]) == self.comm.rank and int(f[1]) == sweeps:
+            print(f"[svdj] fault injection: rank {self.comm.rank} exits after sweep {sweeps}",
+                  file=sys.stderr, flush=True)
+            import os
+            os._exit(17)
 
     def _chain_streams(self, dev):
         """The chain streams are created ONCE per solver and reused: torch
@@ -424,7 +449,7 @@ class DistributedBlockJacobi(Solver):
             Ad = A.to(device=At.device, dtype=At.dtype)
             sends = []
             for dst in range(comm.world):
-                buf = torch.zeros_like(At) if dst != 0 else At
+                buf = torch.zeros_like(At[:2 * B]) if dst != 0 else At
                 for s in range(2):
                     sb = int(tour.held[0, dst, s])
                     c0, c1 = sb * B, min((sb + 1) * B, n)
@@ -434,7 +459,7 @@ class DistributedBlockJacobi(Solver):
                     sends.append((buf, dst))
             comm.sendrecv(sends, [])
         else:
-            comm.sendrecv([], [(At, 0)])
+            comm.sendrecv([], [(At[:2 * B], 0)])
 
     def roundtrip(self, A: torch.Tensor | None, m: int, n: int, dtype=torch.float64):
         """Scatter root-owned A over the ranks' resident super-blocks and gather

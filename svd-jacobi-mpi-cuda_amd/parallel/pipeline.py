@@ -206,34 +206,131 @@ def _global_block(place_g, b: int, k: int, h: int) -> int:
     return sb * k + hh * h + off
 
 
+def _union(iv: list) -> list:
+    """Sorted, merged union of (start, end) intervals."""
+    out = []
+    for a, b in sorted(x for x in iv if x[1] > x[0]):
+        if out and a <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return out
+
+
+def exposed_time(waits: list, busy: list) -> float:
+    """Measure of the time covered by some wait interval (a compute stream
+    idle until an exchange arrives) and by NO busy interval (a task running
+    on any compute stream of the rank): each moment counts once, however many
+    consumers wait on the arrival and on however many streams."""
+    w, b = _union(waits), _union(busy)
+    total, j = 0.0, 0
+    for ws, we in w:
+        t = ws
+        while j < len(b) and b[j][1] <= t:
+            j += 1
+        k = j
+        while t < we:
+            if k < len(b) and b[k][0] <= t:
+                t = max(t, b[k][1])
+                k += 1
+                continue
+            nxt = b[k][0] if k < len(b) else we
+            total += min(nxt, we) - t
+            t = min(nxt, we)
+    return total
+
+
+class HalfLayout:
+    """Where each resident half super-block lives: the rank's storage is a
+    row of half buffers (hB columns each): loc[slot][half] is the buffer of
+    (slot, half), spare[half] the free buffer that the next exchange of a
+    half ``half`` receives into.  An exchange sends from loc[x][h], receives
+    into spare[h] and swaps the two -- the received columns are used where
+    they landed, no copy (round 2 received into a staging buffer and copied
+    it into place: 654 copy dispatches per 8-GPU rank-plan profile).
+    Buffers {h, 2 + h, 4 + h} always hold (slot 0, h), (slot 1, h), spare."""
+
+    def __init__(self, spares: bool):
+        self.loc = [[0, 1], [2, 3]]
+        self.spare = [4, 5] if spares else None
+
+    @property
+    def nbuf(self) -> int:
+        return 6 if self.spare is not None else 4
+
+    def canonical(self) -> bool:
+        return self.loc == [[0, 1], [2, 3]]
+
+    def table(self, k: int) -> np.ndarray:
+        """Local block id (slot * k + half * k/2 + j) -> physical block id."""
+        hk = k // 2
+        t = np.empty(2 * k, dtype=np.int32)
+        for s in range(2):
+            for h in range(2):
+                t[s * k + h * hk:s * k + (h + 1) * hk] = self.loc[s][h] * hk + np.arange(hk)
+        return t
+
+    def moves_to_canonical(self) -> list:
+        """(src buffer, dst buffer) copies that bring (slot, half) back to
+        buffer 2 slot + half, using the spare as scratch (applied in order)."""
+        mv = []
+        if self.spare is None:
+            return mv
+        for h in range(2):
+            where = {0: self.loc[0][h], 1: self.loc[1][h]}  # slot -> buffer
+            free = self.spare[h]
+            for _ in range(4):
+                todo = [s for s in (0, 1) if where[s] != 2 * s + h]
+                if not todo:
+                    break
+                ready = [s for s in todo if 2 * s + h == free]
+                if ready:
+                    s = ready[0]
+                    mv.append((where[s], free))
+                    where[s], free = free, where[s]
+                else:  # both slots sit in each other's home: park one in the spare
+                    s = todo[0]
+                    mv.append((where[s], free))
+                    where[s], free = free, where[s]
+            self.loc[0][h], self.loc[1][h], self.spare[h] = where[0], where[1], free
+        return mv
+
+
 class PipelineExecutor:
     """Runs a :class:`SweepPlan` on the resident buffers of one rank.
+
+    Storage: ``At``/``Vt``/``D`` hold :class:`HalfLayout` ``nbuf`` half
+    buffers (4, or 6 with the two receive spares of a multi-rank job); the
+    plan's local block ids are mapped to buffers at issue time.  Call
+    :meth:`canonicalize` before reading the result: it moves the halves back
+    to buffer 2 slot + half, i.e. rows [s B, (s+1) B) = slot s.
 
     Exchange timing (``timing=True``, device runs with a stream-ordered
     communicator): every half exchange is bracketed on the comm stream by two
     timing events (issue after its producers' events, arrival of both
-    directions), and every consumer records an event on its own stream just
-    before it starts waiting for the arrival.  :meth:`comm_summary` turns them
-    into ``comm_ms`` (sum of exchange spans, including waiting for the peer)
-    and ``exposed_comm_ms`` (sum over consumers of how long the arrival
-    trailed the moment the consumer stream was ready -- the part of the
-    exchange not hidden under compute)."""
+    directions); every task is bracketed on its stream (start after its waits,
+    end), and every consumer records an event just before it waits for an
+    arrival.  :meth:`comm_summary` reports ``comm_ms`` (sum of exchange
+    spans) and ``exposed_comm_ms``: the time during which some compute stream
+    waited for an arrival while no task ran on any compute stream
+    (:func:`exposed_time`) -- the part of the exchanges on the critical path."""
 
     def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour, timing: bool = False,
                  parts: int = 2):
+        if parts != 2:
+            raise ValueError("the pipelined executor moves super-blocks in halves")
         self.comm, self.streams = comm, streams
         self.At, self.Vt, self.D = At, Vt, D
         self.k, self.W, self.tour = k, W, tour
         self.parts = parts
         self.hB = k // parts * W
+        self.layout = HalfLayout(spares=comm.distributed)
+        if At.shape[0] != self.layout.nbuf * self.hB or D.shape[0] != At.shape[0]:
+            raise ValueError(f"storage must hold {self.layout.nbuf} half buffers of {self.hB} "
+                             f"columns, got {At.shape[0]}")
         dev = At.device
         self.cuda = dev.type == "cuda"
-        hB = self.hB
-        self.rbuf = [(torch.empty(hB, At.shape[1], dtype=At.dtype, device=dev),
-                      torch.empty(hB, Vt.shape[1], dtype=Vt.dtype, device=dev) if Vt is not None
-                      else None,
-                      torch.empty(hB, dtype=D.dtype, device=dev)) for _ in range(parts)]
-        self.dev_pairs = {}  # item index -> device pairs (the plan is fixed per solve)
+        self.dev_pairs = {}  # (item index, buffers of its halves) -> device pairs
         self._groups = {}
         self.comm_stream = torch.cuda.Stream(dev) if self.cuda and comm.distributed else None
         self.stream_ordered = self.cuda and getattr(comm, "async_device", False)
@@ -241,18 +338,30 @@ class PipelineExecutor:
         self._t0 = None
         self._spans = []     # (issue event, arrival event) per half exchange
         self._waits = []     # (consumer-ready event, arrival event) per consume
+        self._busy = []      # (start event, end event) per task
         self.bytes_sent = 0
 
-    def _rows(self, slot: int, half: int) -> slice:
-        b0 = slot * self.k * self.W + half * self.hB
-        return slice(b0, b0 + self.hB)
+    @staticmethod
+    def storage_columns(B: int, distributed: bool) -> int:
+        """Columns (rows of At) a rank allocates: 2B, plus a spare half per
+        half index when exchanges happen."""
+        return (3 if distributed else 2) * B
+
+    def _buf(self, b: int) -> slice:
+        return slice(b * self.hB, (b + 1) * self.hB)
 
     def _pairs(self, i: int, task: Task):
-        t = self.dev_pairs.get(i)
+        bufs = tuple(self.layout.loc[s][h] for s, h in task.halves)
+        key = (i, bufs)
+        t = self.dev_pairs.get(key)
         if t is None:
-            t = torch.from_numpy(task.pairs).to(self.At.device)
-            self.dev_pairs[i] = t
+            phys = self.layout.table(self.k)[task.pairs]
+            t = torch.from_numpy(np.ascontiguousarray(phys)).to(self.At.device)
+            self.dev_pairs[key] = t
         return t
+
+    def _event(self):
+        return torch.cuda.Event(enable_timing=self.timing)
 
     def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
@@ -273,7 +382,7 @@ class PipelineExecutor:
             for s in self.streams + ([self.comm_stream] if self.comm_stream else []):
                 s.wait_event(ready)
         last = {}       # (slot, half) -> [events of tasks since last exchange]
-        pending = {}    # (slot, half) -> (works, buffers) received, not yet copied
+        pending = {}    # (slot, half) -> arrival event / works, not yet waited for
         t_comm = 0.0
         halves_done = {}
         index = {id(it): i for i, it in enumerate(plan.items)}
@@ -291,13 +400,14 @@ class PipelineExecutor:
                 t_comm += time.perf_counter() - tc
                 continue
             tasks = it if isinstance(it, tuple) else (it,)
-            pairs = [self._pairs(index[id(t)], t) for t in tasks]
             if not self.cuda:
-                for t, pr in zip(tasks, pairs):
+                for t in tasks:
                     for hv in t.halves:
                         self._consume(hv, pending)
-                    run_steps(pr, t.modes, t.stream)
+                    run_steps(self._pairs(index[id(t)], t), t.modes, t.stream)
                 continue
+            pairs = [self._pairs(index[id(t)], t) for t in tasks]
+            starts = []
             for t in tasks:  # dependencies, on each task's own stream
                 s = self.streams[t.stream]
                 with torch.cuda.stream(s):
@@ -305,6 +415,10 @@ class PipelineExecutor:
                         for ev in last.get(hv, ()):
                             s.wait_event(ev)
                         self._consume(hv, pending)
+                    if self.timing:
+                        st = self._event()
+                        st.record(s)
+                        starts.append(st)
             if len(tasks) == 2:
                 a, b = tasks
                 run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
@@ -312,14 +426,16 @@ class PipelineExecutor:
             else:
                 with torch.cuda.stream(self.streams[tasks[0].stream]):
                     run_steps(pairs[0], tasks[0].modes, tasks[0].stream)
-            for t in tasks:
-                ev = torch.cuda.Event()
+            for q, t in enumerate(tasks):
+                ev = self._event()
                 ev.record(self.streams[t.stream])
+                if self.timing:
+                    self._busy.append((starts[q], ev))
                 for hv in t.halves:
                     last.setdefault(hv, []).append(ev)
         if self.cuda:
             main = torch.cuda.current_stream(self.At.device)
-            for s in self.streams:
+            for s in self.streams + ([self.comm_stream] if self.comm_stream else []):
                 main.wait_stream(s)
         return t_comm
 
@@ -328,19 +444,20 @@ class PipelineExecutor:
         g = comm.rank
         r, x, hh = it.round, it.slot, it.half
         dst, src = int(tour.send_to[r, g]), int(tour.recv_from[r, g])
-        sl = self._rows(x, hh)
-        rA, rV, rD = self.rbuf[hh]
-        sends = [(self.At[sl], dst), (self.D[sl], dst)]
-        recvs = [(rA, src), (rD, src)]
+        out_b, in_b = self.layout.loc[x][hh], self.layout.spare[hh]
+        so, si = self._buf(out_b), self._buf(in_b)
+        sends = [(self.At[so], dst), (self.D[so], dst)]
+        recvs = [(self.At[si], src), (self.D[si], src)]
         if self.Vt is not None:
-            sends.append((self.Vt[sl], dst))
-            recvs.append((rV, src))
+            sends.append((self.Vt[so], dst))
+            recvs.append((self.Vt[si], src))
         self.bytes_sent += sum(t.numel() * t.element_size() for t, _ in sends)
         if not comm.distributed:
             raise RuntimeError("exchange on a single rank")
+        # from here on (host program order) the half lives in the received buffer
+        self.layout.loc[x][hh], self.layout.spare[hh] = in_b, out_b
         if not self.cuda:
             comm.sendrecv(sends, recvs)
-            self._copy_in(sl, hh)
             last.pop((x, hh), None)
             return
         cs = self.comm_stream
@@ -357,6 +474,8 @@ class PipelineExecutor:
         # Stream-ordered (RCCL): the comm stream issues the grouped send/recv
         # after the producers' events, then waits (device-side) for both
         # directions; consumers wait on ONE arrival event -- no host sync.
+        # The receive buffer's last readers were waited for by the exchange
+        # that freed it, earlier on this same stream.
         with torch.cuda.stream(cs):
             t_issue = None
             if self.timing:
@@ -364,7 +483,7 @@ class PipelineExecutor:
                 t_issue.record(cs)
             for w in comm.isendrecv(sends, recvs):
                 w.wait()
-            arrived = torch.cuda.Event(enable_timing=self.timing)
+            arrived = self._event()
             arrived.record(cs)
         if self.timing:
             self._spans.append((t_issue, arrived))
@@ -386,7 +505,14 @@ class PipelineExecutor:
                 w.wait()  # gloo: blocks the host until both directions are done
             if self.cuda:
                 torch.cuda.synchronize(self.At.device)
-        self._copy_in(self._rows(*hv), hv[1])
+
+    def canonicalize(self):
+        """Move every half back to buffer 2 slot + half (enqueued on the
+        current stream, which :meth:`run` made wait for every other stream)."""
+        for src, dst in self.layout.moves_to_canonical():
+            for t in (self.At, self.Vt, self.D):
+                if t is not None:
+                    t[self._buf(dst)].copy_(t[self._buf(src)])
 
     def comm_summary(self) -> dict:
         """Exchange timing of every sweep run so far (synchronises)."""
@@ -394,20 +520,15 @@ class PipelineExecutor:
         if not self.timing or self._t0 is None:
             return out
         torch.cuda.synchronize(self.At.device)
-        out["comm_ms"] = round(sum(a.elapsed_time(b) for a, b in self._spans), 3)
         t0 = self._t0
-        exposed = 0.0
-        for ready, arrived in self._waits:
-            exposed += max(0.0, t0.elapsed_time(arrived) - t0.elapsed_time(ready))
-        out["exposed_comm_ms"] = round(exposed, 3)
+        out["comm_ms"] = round(sum(a.elapsed_time(b) for a, b in self._spans), 3)
+        waits = [(t0.elapsed_time(r), t0.elapsed_time(a)) for r, a in self._waits]
+        busy = [(t0.elapsed_time(a), t0.elapsed_time(b)) for a, b in self._busy]
+        out["exposed_comm_ms"] = round(exposed_time(waits, busy), 3)
+        # the round-2 figure (sum over consumers of arrival - consumer ready),
+        # which double-counts shared arrivals and waits under other compute
+        out["consumer_wait_sum_ms"] = round(sum(max(0.0, b - a) for a, b in waits), 3)
         return out
-
-    def _copy_in(self, sl, hh):
-        rA, rV, rD = self.rbuf[hh]
-        self.At[sl].copy_(rA)
-        self.D[sl].copy_(rD)
-        if self.Vt is not None:
-            self.Vt[sl].copy_(rV)
 
     def _update_phys(self, r: int, phys):
         tour, P = self.tour, self.comm.world

@@ -13,9 +13,13 @@ from svdj.parallel import Communicator, DistributedBlockJacobi  # noqa: E402
 def main():
     m, n, W, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     mode = sys.argv[5] if len(sys.argv) > 5 else "root"
-    comm = Communicator(backend="gloo", device=torch.device("cpu"))
+    comm = Communicator(backend="gloo", device=torch.device("cpu"),
+                        timeout_s=float(os.environ.get("SVDJ_TEST_TIMEOUT", "600")))
     cfg = svdj.SolverConfig(block=W, dtype=torch.float64, max_inner_sweeps=1,
                             precondition="qr" if "qr" in mode else "none")
+    if mode == "fault":  # rank 1 dies after sweep 1; rank 0 must fail, not hang
+        cfg.extra["fault_exit"] = (1, 1)
+        mode = "root"
     solver = DistributedBlockJacobi(cfg, comm)
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=9)
     if mode == "roundtrip":  # reference test_local_matrix_distribution_* parity

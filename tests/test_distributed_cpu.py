@@ -105,3 +105,34 @@ def test_row_distributed_cholqr2(world, tmp_path):
     assert rep["converged"] and rep["world"] == world
     assert rep["residual_rel"] < 1e-12 and rep["orth_u_fro"] < 1e-10, rep
     assert rep["orth_v_fro"] < 1e-10 and rep["sigma_err"] < 1e-12, rep
+
+
+def test_dead_peer_fails_survivor_fast(tmp_path):
+    """Failure detection, Python engine: rank 1 exits
+    abruptly after sweep 1 (SolverConfig.extra fault_exit, like a crashed
+    peer).  The ranks are started directly, not by torchrun (whose agent
+    would kill the survivor itself): rank 0 must exit non-zero on its own,
+    well within the communicator timeout, instead of hanging."""
+    import time
+    port = _free_port()
+    out = tmp_path / "fault.json"
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, OMP_NUM_THREADS="1", RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   SVDJ_TEST_TIMEOUT="60")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(HERE, "_dist_worker.py"), "200", "192", "32", str(out),
+             "fault"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        outs = [p.communicate(timeout=180) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    el = time.time() - t0
+    assert procs[1].returncode == 17, outs[1][1][-2000:]
+    assert procs[0].returncode not in (0, None), outs[0][1][-2000:]
+    assert el < 120, el
+    assert not out.exists()

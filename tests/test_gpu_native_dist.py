@@ -60,3 +60,35 @@ def test_native_dist_rank_failure_stops_job():
     r = subprocess.run([_exe(), "256", "--np", "2", "--shared-gpu", "--block", "48",
                         "--timeout", "60"], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
+
+
+def test_native_dead_peer_watchdog():
+    """Failure detection, native engine: rank 1 exits abruptly after sweep 2
+    (--inject-fault 1:2) and the launcher does NOT stop the other rank
+    (--keep-going), so rank 0's own watchdog (RCCL async error, or no sweep
+    finished within --timeout) must abort its communicator and exit 3 --
+    within the timeout, not hang in a receive from the dead peer."""
+    import time
+    t0 = time.time()
+    r = subprocess.run([_exe(), "1024", "--np", "2", "--shared-gpu", "--dtype", "f32",
+                        "--input", "dense", "--inject-fault", "1:2", "--keep-going",
+                        "--timeout", "20"], capture_output=True, text=True, timeout=150)
+    el = time.time() - t0
+    out = r.stdout + r.stderr
+    assert r.returncode != 0, out[-3000:]
+    assert "fault injection: rank 1" in out, out[-3000:]
+    assert "[rank 0]" in out and "watchdog" in out.lower(), out[-3000:]
+    assert el < 110, (el, out[-3000:])
+
+
+def test_native_persistent_handle_repeat_solves():
+    """Warm-up solves reuse the persistent handle (no per-solve allocation):
+    the timed solve after two warm-ups converges to the same accuracy, with
+    the exchange timing reported (receive in place, no copy-in)."""
+    r = subprocess.run([_exe(), "1024", "--np", "2", "--shared-gpu", "--dtype", "f32",
+                        "--input", "dense", "--verify", "--warmup", "2", "--comm-timing",
+                        "--timeout", "120"], capture_output=True, text=True, timeout=170)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "converged: 1" in out and "exposed_comm_ms:" in out, out
+    assert _value(out, "||A-USVt||_F/||A||_F:") < 2e-5, out

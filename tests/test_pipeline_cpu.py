@@ -159,3 +159,44 @@ def test_chain_count_validated():
             svdj.SolverConfig(chains=bad)
     with pytest.raises(ValueError):
         pipeline.sweep_plan(2, 4, schedule.tournament(2).xslot[:, 0], chains=4)
+
+
+def test_half_layout_receive_in_place_and_canonicalize():
+    """Exchanges receive into the spare of their half index and swap; after
+    any exchange sequence the canonicalising moves bring every (slot, half)
+    back to buffer 2 slot + half, never overwriting live data."""
+    import random
+    rnd = random.Random(3)
+    for trial in range(200):
+        lay = pipeline.HalfLayout(spares=True)
+        content = {b: None for b in range(6)}  # buffer -> (slot, half) data tag
+        for s in range(2):
+            for h in range(2):
+                content[lay.loc[s][h]] = (s, h, 0)
+        gen = {(s, h): 0 for s in range(2) for h in range(2)}
+        for _ in range(rnd.randrange(0, 12)):
+            x, h = rnd.randrange(2), rnd.randrange(2)
+            out_b, in_b = lay.loc[x][h], lay.spare[h]
+            assert {lay.loc[0][h], lay.loc[1][h], lay.spare[h]} == {h, 2 + h, 4 + h}
+            gen[(x, h)] += 1
+            content[in_b] = (x, h, gen[(x, h)])   # the received replacement
+            lay.loc[x][h], lay.spare[h] = in_b, out_b
+        want = {(s, h): content[lay.loc[s][h]] for s in range(2) for h in range(2)}
+        for src, dst in lay.moves_to_canonical():
+            content[dst] = content[src]
+        assert lay.canonical()
+        for s in range(2):
+            for h in range(2):
+                assert content[2 * s + h] == want[(s, h)]
+
+
+def test_exposed_time_counts_each_moment_once():
+    """exposed_time: a wait counts only while no task runs on any stream, and
+    overlapping waits (two consumers of one arrival) count once."""
+    ex = pipeline.exposed_time
+    assert ex([(0, 10)], []) == 10
+    assert ex([(0, 10), (2, 10)], []) == 10            # two consumers, one arrival
+    assert ex([(0, 10)], [(0, 4), (6, 8)]) == 4        # other stream busy 6 of 10
+    assert ex([(0, 10)], [(-5, 20)]) == 0              # fully hidden
+    assert ex([(0, 3), (5, 8)], [(2, 6)]) == 4
+    assert ex([], [(0, 1)]) == 0
