@@ -91,12 +91,17 @@ def verify_distributed(res, gen, m, n, comm, dtype):
     del Uall, Vall
     eye_rows = torch.zeros(len(glob), n, dtype=dtype, device=dev)
     eye_rows[torch.arange(len(glob), device=dev), gidx] = 1
+    EV = V.t() @ Vfull.t() - eye_rows
+    EU = U.t() @ Ufull.t() - eye_rows
     parts = torch.stack([R.double().pow(2).sum(), A.double().pow(2).sum() / comm.world,
-                         (V.t() @ Vfull.t() - eye_rows).double().pow(2).sum(),
-                         (U.t() @ Ufull.t() - eye_rows).double().pow(2).sum()])
+                         EV.double().pow(2).sum(), EU.double().pow(2).sum()])
     parts = comm.allreduce_sum_(parts.to(comm_device(comm, dev))).cpu()
+    # largest single entry |u_i^T u_j - delta_ij|: the stop test bounds the
+    # final couplings by tol (sqrt(m) eps), so the Frobenius norm grows ~ n tol
+    mx = comm.allgather(torch.stack([EU.abs().max(), EV.abs().max()]).double()).cpu().amax(0)
     return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
             "orth_v_fro": float(parts[2].sqrt()), "orth_u_fro": float(parts[3].sqrt()),
+            "orth_u_max_abs": float(mx[0]), "orth_v_max_abs": float(mx[1]),
             "orth_scope": "full n x n Gram (all-gathered)"}
 
 
