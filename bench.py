@@ -228,7 +228,7 @@ def simulate(a, cfg, dtype, work):
         "simulated_P": P, "simulated_rank": g, "sweeps_run": res.sweeps,
         "solve_s": round(el, 4), "dtype": a.dtype,
         "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
-                   "chains": a.chains, "inner_order": a.inner_order,
+                   "chains": a.chains, "inner_order": res.info.get("inner_order", a.inner_order),
                    "link_gbps_model": a.sim_link_gbps},
         "comm": res.info.get("comm"),
         "qr_seconds": res.info.get("qr_seconds"),
@@ -352,7 +352,7 @@ def run_native(a, dtype, work):
     p.At, p.Vt, p.D = At.data_ptr(), Vt.data_ptr(), D.data_ptr()
     p.tol = a.tol if a.tol is not None else default_tol(dtype, m)
     p.tol_mode, p.max_sweeps, p.mma = 0, a.max_sweeps, 0
-    p.inner_order = 1 if a.inner_order == "bipartite" else 0
+    p.inner_order = {"cyclic": 0, "bipartite": 1, "cross": 2, "auto": 3}[a.inner_order]
     p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
     p.hist = C.cast(hist, C.POINTER(C.c_double))
     p.stagger = 1 if a.stagger else 0
@@ -477,7 +477,8 @@ def main():
     p.add_argument("--tol", type=float, default=None,
                    help="rotation threshold (default sqrt(m) eps of the problem dtype)")
     p.add_argument("--chains", type=int, default=2, choices=[1, 2])
-    p.add_argument("--inner-order", default=svdj_default_inner(), choices=["cyclic", "bipartite"],
+    p.add_argument("--inner-order", default=svdj_default_inner(),
+                   choices=["auto", "cyclic", "bipartite", "cross"],
                    help="EVD ordering of the block cross steps")
     p.add_argument("--stagger", dest="stagger", action="store_true", default=None,
                    help="offset the two step chains by an EVD (svdj_block_steps2)")
@@ -632,7 +633,7 @@ def main():
                 "mma": last.info.get("mma", a.mma),
                 "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
-                "inner_order": a.inner_order,
+                "inner_order": last.info.get("inner_order", a.inner_order),
                 "staggered": bool(a.stagger),
                 "root_owned": a.root_owned,
             },

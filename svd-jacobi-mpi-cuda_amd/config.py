@@ -50,8 +50,10 @@ class SolverConfig:
     tol_mode: str = "relative"      # relative | absolute (reference parity)
     max_sweeps: int = 60            # reference: 1 (main.cu:482)
     max_inner_sweeps: int = 1       # block path: Jacobi sweeps per pair EVD (1 = one pass)
-    inner_order: str = "bipartite"  # block path, cross steps: cyclic (2W-1 EVD steps, all
-                                    # pairs) | bipartite (W steps, cross pairs only)
+    inner_order: str = "auto"       # block path, cross steps: cyclic (2W-1 EVD steps, all
+                                    # pairs) | bipartite (W steps, cross pairs only) |
+                                    # cross (bipartite steps, only the cross couplings
+                                    # tracked) | auto (models.block.choose_inner_order)
     ordering: str = "sameh"         # scalar path: sameh (reference) | round_robin
     rotation: str = "schur"         # oracle: schur (reference inline) | ordered (lib/Utils.cu)
     sort: bool = False              # reference returns unsorted sigma
@@ -118,7 +120,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--tol-mode", default="relative", choices=["relative", "absolute"])
     p.add_argument("--max-sweeps", type=int, default=60)
     p.add_argument("--max-inner-sweeps", type=int, default=1)
-    p.add_argument("--inner-order", default=None, choices=["cyclic", "bipartite"],
+    p.add_argument("--inner-order", default=None,
+                   choices=["auto", "cyclic", "bipartite", "cross"],
                    help="EVD ordering of the block cross steps (default: the config's)")
     p.add_argument("--ordering", default="sameh", choices=["sameh", "round_robin"])
     p.add_argument("--sort", action="store_true")

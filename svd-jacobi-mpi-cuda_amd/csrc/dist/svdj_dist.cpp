@@ -545,7 +545,9 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   auto guard = [&](int r) {
     if (r < 0 && !rc) rc = r;
   };
-  guard(build_templates(h, p->inner_order ? 2 : 0));
+  // 3 = auto: by the pairs of a cross step (half super-blocks)
+  const int io = p->inner_order == 3 ? svdj_choose_inner_order(W, h->hk) : p->inner_order;
+  guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
   for (int c = 0; c < 2 && !rc; ++c)
     if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);

@@ -5,7 +5,8 @@
 //
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
-//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite] [--no-v]
+//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
+//                  [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH] [--comm-timing] [--inject-fault RANK:SWEEP] [--keep-going]
 //
@@ -53,7 +54,7 @@
 namespace {
 
 struct Opts {
-  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 1;
+  int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 3;  // auto
   int fault_rank = -1, fault_sweep = -1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
@@ -366,7 +367,10 @@ int main(int argc, char** argv) {
     else if (a == "--verify") o.verify = true;
     else if (a == "--timeout") o.timeout = std::atof(next());
     else if (a == "--warmup") o.warmup = std::atoi(next());
-    else if (a == "--inner") o.inner = std::string(next()) == "bipartite" ? 1 : 0;
+    else if (a == "--inner") {
+      const std::string v = next();
+      o.inner = v == "auto" ? 3 : (v == "cross" ? 2 : (v == "bipartite" ? 1 : 0));
+    }
     else if (a == "--id-file") o.id_file = next();
     else if (a == "--comm-timing") o.comm_timing = true;
     else if (a == "--keep-going") o.keep_going = true;

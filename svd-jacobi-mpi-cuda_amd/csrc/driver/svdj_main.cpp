@@ -144,7 +144,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s N [--m M] [--input triu|dense] [--dtype f32|f64] ...\n", argv[0]);
     return 1;
   }
-  int n = std::atoi(argv[1]), m = n, W = 0, max_sweeps = 60, inner_order = 1;
+  int n = std::atoi(argv[1]), m = n, W = 0, max_sweeps = 60, inner_order = 3;  // auto
   unsigned seed = 1000000;
   double tol = -1;
   bool verify = false;
@@ -161,7 +161,10 @@ int main(int argc, char** argv) {
     else if (a == "--max-sweeps") max_sweeps = std::atoi(next());
     else if (a == "--tol") tol = std::atof(next());
     else if (a == "--mma") mma = next();
-    else if (a == "--inner") inner_order = std::string(next()) == "bipartite" ? 1 : 0;
+    else if (a == "--inner") {
+      const std::string v = next();
+      inner_order = v == "auto" ? 3 : (v == "cross" ? 2 : (v == "bipartite" ? 1 : 0));
+    }
     else if (a == "--verify") verify = true;
     else if (a == "--report-dir") report_dir = next();
     else if (a == "--no-report") report_dir.clear();

@@ -979,6 +979,336 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
 }
 
+// ----------------------------------------- evd, cross-only bipartite (mode 3)
+// The EVD of a cross step that tracks only what the bipartite ordering
+// reads: the W x W cross couplings C and the 2W diagonals.  When a cross
+// step starts, each block's own columns are mutually orthogonal (the
+// full-Gram step that opens every sweep rotates the within-block pairs), so
+// G = [[Dx, C], [C^T, Dy]].  A rotation of (x_i, y) creates within-block
+// couplings only at first order in its sine, and those feed back into the
+// cross couplings at second order: the update
+//   C'[i][j] = c_i c_k C[i][j] - s_i s_k C[k][pi(i)]     (y_j paired with x_k)
+// drops them.  Near convergence the sines are tiny and the rotations are the
+// exact ones; early on they differ slightly, which the next outer visit of
+// the pair re-measures from the data.  CPU emulation (fp32 / fp64, n = 512 /
+// 1024, W = 32 / 64): the same sweep counts as the full bipartite EVD +-1,
+// the same accuracy.
+//
+// Position space: at step t, Y position p holds y_{(p + t) mod W}; slot a
+// pairs x_a with position a.  E[i][p] = C[i][y at p].  The update pairs
+// E[i][p] with E[p][i] (a STATIC transpose pair) and the new values move
+// one position left: E_{t+1}[i][p] = E'_t[i][p+1].  Groups {E[i][i+d],
+// E[i+d][i]} along diagonals d = 1..W/2:
+//   * wave 0, lane a = slot a, holds d = 1 and d = 2 in REGISTERS: its next
+//     active coupling E_{t+1}[a][a] = E'_t[a][a+1] needs only values of
+//     lanes a+1 and a+2 (their rotations, E_t[a+1][a] = lane a+1's settled
+//     coupling, E_t[a+2][a] = lane a+1's previous d = 1 result), fetched
+//     with DPP lane rotates -- the solve chain has no LDS read on it;
+//   * waves 1.. hold d = 3..W/2 in LDS (row stride W, bank-conflict-free),
+//     two diagonals per wave; the d = 2 / d = 3 values cross through LDS.
+// ONE barrier per step.  The kernel does not accumulate Q: every step's
+// rotations go to global memory as fp64 (c, s) records, and qbuild_kernel
+// forms Q = J_0 J_1 ... row-parallel on many CUs (rows of Q evolve
+// independently).  Measured in isolation (tools/micro/evd_bench.hip, 8
+// pairs, W = 64): register Q accumulation and the solve chain made the
+// per-step time ~2000 cycles; the G update itself was not the limit.
+template <int W>
+__host__ __device__ constexpr int cross_threads() { return W == 64 ? 1024 : 512; }
+constexpr int kCrossMaxInner = 4;  // inner sweeps whose rotation records fit the workspace
+
+template <typename T, int W>
+__global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
+    const int32_t* __restrict__ pairs, const T* __restrict__ slabs, int nchunk,
+    T* __restrict__ D, Pair2<double>* __restrict__ rec, int32_t* __restrict__ nsteps,
+    int32_t* __restrict__ skip, T tol, int absmode, int max_inner, uint32_t* __restrict__ metric) {
+  static_assert(W == 32 || W == 64, "cross EVD: W = 32 or 64");
+  constexpr int NT = cross_threads<W>();
+  constexpr int NWAVE = NT / SVDJ_WAVE;
+  static_assert(NWAVE - 1 == (W / 2 - 2) / 2, "two diagonals per wave >= 1");
+  constexpr int N = 2 * W;
+  using T2 = Pair2<T>;
+  using Q2 = Pair2<double>;
+
+  __shared__ T Eb[2][W * W];  // cross couplings by (x slot, y position), double-buffered
+  __shared__ T dg[N];
+  __shared__ T2 rcs[2][W];
+  __shared__ int rot_flag[2];
+  __shared__ float wmax[NWAVE];
+  __shared__ int wneed[NWAVE];
+  __shared__ int need_any;
+
+  const int pair = blockIdx.x;
+  const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- assemble: diagonals from D, E_0[i][p] = C[i][p] (split-K slabs
+  // summed in fp64), convergence value and the "anything to rotate" test
+  for (int a = tid; a < N; a += NT) dg[a] = D[a < W ? bi * W + a : bj * W + (a - W)];
+  __syncthreads();
+  {
+    float mx = 0.0f;
+    int need = 0;
+    constexpr int EV = 16 / (int)sizeof(T);
+    const T* s0 = slabs + (size_t)pair * nchunk * (W * W);
+    for (int gi = tid; gi < W * W / EV; gi += NT) {
+      double acc[EV];
+#pragma unroll
+      for (int u = 0; u < EV; ++u) acc[u] = 0.0;
+#pragma unroll SVDJ_EVD_SLAB_UNROLL
+      for (int k = 0; k < nchunk; ++k) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(s0 + (size_t)k * W * W + gi * EV);
+        const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+        for (int u = 0; u < EV; ++u) acc[u] += (double)e[u];
+      }
+#pragma unroll
+      for (int u = 0; u < EV; ++u) {
+        const int i = gi * EV + u;
+        const T g = (T)acc[u];
+        Eb[0][i] = g;
+        const T grr = dg[i / W], gcc = dg[W + i % W];
+        const T d = sqrt(grr) * sqrt(gcc);
+        if (d > T(0)) {
+          const float v = (float)(fabs(g) / d);
+          mx = v > mx ? v : mx;
+        }
+        need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
+      }
+    }
+    mx = wave_max(mx);
+    need = __any(need) ? 1 : 0;
+    if (lane == 0) {
+      wmax[wave] = mx;
+      wneed[wave] = need;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float m2 = 0.0f;
+      int n2 = 0;
+      for (int w = 0; w < NWAVE; ++w) {
+        m2 = wmax[w] > m2 ? wmax[w] : m2;
+        n2 |= wneed[w];
+      }
+      atomic_max_pos(&metric[0], m2);
+      need_any = n2;
+    }
+    __syncthreads();
+  }
+  const bool run = need_any != 0;
+  const int inner = max_inner < kCrossMaxInner ? max_inner : kCrossMaxInner;
+
+  // ---- LDS groups of waves >= 1: (i, d), d = 2w+1, 2w+2 (W = 64: both on
+  // every lane; W = 32: lanes 0..31 the first, 32..63 the second)
+  int gi[2] = {0, 0}, gp[2] = {0, 0}, rd0[2], rd1[2], wr0[2], wr1[2];
+  int ng = 0;
+  auto add_group = [&](int i, int d) {
+    if (d == W / 2 && i >= W / 2) return;  // the half diagonal has W/2 groups
+    const int p = (i + d) % W;
+    gi[ng] = i;
+    gp[ng] = p;
+    rd0[ng] = i * W + p;
+    rd1[ng] = p * W + i;
+    wr0[ng] = i * W + (p + W - 1) % W;
+    wr1[ng] = p * W + (i + W - 1) % W;
+    ++ng;
+  };
+  if (wave >= 1) {
+    if constexpr (W == 64) {
+      add_group(lane, 2 * wave + 1);
+      add_group(lane, 2 * wave + 2);
+    } else {
+      add_group(lane & 31, 2 * wave + 1 + (lane >> 5));
+    }
+  }
+
+  // ---- solver lanes (wave 0, lane a < W): slot a's state in registers
+  const bool solver = wave == 0 && lane < W;
+  const int a = lane % W;
+  T rc = T(1), rs = T(0);   // rotation of slot a at the current step
+  T rdx = T(0), rdy = T(0); // x_a / y at position a after the current step's rotation
+  T pend = T(0);            // slot a's coupling after the current step's rotation
+  T pend_prev = T(0);       // ... after the previous step: E_t[a][a-1]
+  T g1 = T(0);              // E_t[a][a+1]
+  T h2src = T(0);           // E_t[a+1][a-1] (lane a-1's E_t[(a-1)+2][a-1])
+  T dx_out = T(0), dy_out = T(0);
+  Q2* rq = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  auto solve = [&](T dx, T dy, T g, int step, bool& rot) {
+    T c, sn, t;
+    rot = rotation_fast(dx, dy, g, tol, absmode, c, sn, t);
+    double c64, s64;
+    if constexpr (sizeof(T) == 8) {
+      c64 = c;
+      s64 = sn;
+    } else {  // fp64 (c, s) of the fp32 t, normalised in fp64 (Q stays orthogonal)
+      const double td = (double)t;
+      c64 = rsqrt64(fma(td, td, 1.0));
+      s64 = td * c64;
+    }
+    if (step < kCrossMaxInner * W) rq[(size_t)step * W + a] = Q2{c64, s64};
+    rc = c;
+    rs = sn;
+    rdx = dx - t * g;
+    rdy = dy + t * g;
+    pend = rot ? T(0) : g;
+  };
+  int racc = 0, racc_next = 0;
+  if (run && solver) {  // step 0 of slot a
+    pend_prev = Eb[0][a * W + (a + W - 1) % W];
+    h2src = Eb[0][((a + 1) % W) * W + (a + W - 1) % W];
+    g1 = Eb[0][a * W + (a + 1) % W];
+    bool rot;
+    solve(dg[a], dg[W + a], Eb[0][a * W + a], 0, rot);
+    racc = rot;
+    rcs[0][a] = T2{rc, rs};
+  }
+  __syncthreads();
+
+  bool any = false;
+  int gs = 0, sw = 0, st = 0;
+  auto step = [&](auto parity) -> bool {
+    constexpr int b = decltype(parity)::value, nb = b ^ 1;
+    const bool last = st + 1 == W;  // this phase solves step 0 of the next inner sweep
+    if (wave == 0) {
+      // neighbours' values (slot a+1, a+2) by lane rotates; E_t[a][a+2] from LDS
+      const T g2 = solver ? Eb[b][a * W + (a + 2) % W] : T(0);
+      const T c1 = bip_shift<W>(rc, a), s1 = bip_shift<W>(rs, a);
+      const T c2 = bip_shift<W>(c1, a), s2 = bip_shift<W>(s1, a);
+      const T h1 = bip_shift<W>(pend_prev, a);  // E_t[a+1][a]
+      const T h2 = bip_shift<W>(h2src, a);      // E_t[a+2][a]
+      const T dyn = bip_shift<W>(rdy, a);       // y at position a+1 after this step
+      if (solver) {
+        const T cc1 = rc * c1, ss1 = rs * s1, cc2 = rc * c2, ss2 = rs * s2;
+        const T n0_1 = cc1 * g1 - ss1 * h1;  // E_{t+1}[a][a]: slot a's next coupling
+        const T n1_1 = cc1 * h1 - ss1 * g1;  // E_{t+1}[a+1][a-1]
+        const T n0_2 = cc2 * g2 - ss2 * h2;  // E_{t+1}[a][a+1]
+        const T n1_2 = cc2 * h2 - ss2 * g2;  // E_{t+1}[a+2][a-1] (a d = 3 group's input)
+        Eb[nb][((a + 2) % W) * W + (a + W - 1) % W] = n1_2;
+        dx_out = rdx;
+        dy_out = rdy;
+        pend_prev = pend;
+        g1 = n0_2;
+        h2src = n1_1;
+        bool rot;
+        solve(rdx, dyn, n0_1, gs + 1, rot);
+        if (last) racc_next |= rot; else racc |= rot;
+        rcs[nb][a] = T2{rc, rs};
+      }
+      if (last) {  // every rotation of inner sweep sw is decided by now
+        const int r = __any(racc) ? 1 : 0;
+        if (lane == 0) rot_flag[sw & 1] = r;
+        racc = racc_next;
+        racc_next = 0;
+      }
+    } else {
+      T e0[2], e1[2];
+      T2 ri[2], rp[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (j < ng) {
+          e0[j] = Eb[b][rd0[j]];
+          e1[j] = Eb[b][rd1[j]];
+          ri[j] = rcs[b][gi[j]];
+          rp[j] = rcs[b][gp[j]];
+        }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (j < ng) {
+          const T cc = ri[j].x * rp[j].x, ss = ri[j].y * rp[j].y;
+          Eb[nb][wr0[j]] = cc * e0[j] - ss * e1[j];
+          Eb[nb][wr1[j]] = cc * e1[j] - ss * e0[j];
+        }
+    }
+    __syncthreads();
+    ++gs;
+    if (++st < W) return false;
+    st = 0;
+    if (!rot_flag[sw & 1]) return true;
+    any = true;
+    return ++sw >= inner;
+  };
+  if (run && inner > 0)
+    while (!step(std::integral_constant<int, 0>{}) && !step(std::integral_constant<int, 1>{})) {
+    }
+
+  if (tid == 0) {
+    skip[pair] = any ? 0 : 1;
+    nsteps[pair] = gs;
+    if (any) atomicAdd(&metric[1], 1u);
+  }
+  if (any && solver) {  // diagonals after the last executed step (gs - 1)
+    D[bi * W + a] = dx_out;
+    D[bj * W + ((a + gs - 1) & (W - 1))] = dy_out;
+  }
+}
+
+// Q = J_0 J_1 ... J_{steps-1} of a cross-step EVD from its fp64 rotation
+// records (evd_cross_kernel), row-parallel: row k of Q evolves on its own
+// (q_k <- q_k J_t), so a pair's 2W rows spread over several workgroups and
+// CUs instead of sitting in the EVD workgroup's registers.  Lane = slot a
+// (W = 32: two slot groups per wave); per row and step one 2x2 fp64 rotation
+// of (Q[k][x_a], Q[k][y at position a]) and a lane rotate of the y column
+// (position a takes what position a+1 held).  The records of up to 64 steps
+// are staged in LDS first with wide loads (one global latency instead of
+// one per step: read step by step from L2 the kernel was latency bound),
+// then read two steps ahead.  Rounded to the data type once, at the end.
+// R rows per lane: 4 when a step has few pairs (latency: more workgroups per
+// pair), 16 with many pairs (throughput: each workgroup stages the pair's
+// records once for 4x the rows).
+constexpr int kQbThreads = 256;
+constexpr int kQbChunk = 64;  // steps staged in LDS at a time
+template <int W, int R>
+__host__ __device__ constexpr int qbuild_blocks() {  // workgroups per pair
+  return (2 * W) / (R * (SVDJ_WAVE / W) * (kQbThreads / SVDJ_WAVE));
+}
+template <typename T, int W, int R>
+__global__ __launch_bounds__(kQbThreads) void qbuild_kernel(
+    const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
+    const int32_t* __restrict__ skip, T* __restrict__ Qall) {
+  constexpr int N = 2 * W;
+  constexpr int GPW = SVDJ_WAVE / W;
+  static_assert(qbuild_blocks<W, R>() * R * GPW * (kQbThreads / SVDJ_WAVE) == N, "row cover");
+  using Q2 = Pair2<double>;
+  __shared__ Q2 rs[kQbChunk * W];
+  const int pair = blockIdx.x;
+  if (skip[pair]) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int a = lane % W;
+  const int k0 = ((blockIdx.y * (kQbThreads / SVDJ_WAVE) + wave) * GPW + lane / W) * R;
+  const int ns = nsteps[pair];
+  const Q2* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  double qx[R], qy[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    qx[i] = (k0 + i == a) ? 1.0 : 0.0;
+    qy[i] = (k0 + i == W + a) ? 1.0 : 0.0;
+  }
+  for (int t0 = 0; t0 < ns; t0 += kQbChunk) {
+    const int nc = ns - t0 < kQbChunk ? ns - t0 : kQbChunk;
+    for (int i = threadIdx.x; i < nc * W; i += kQbThreads) rs[i] = rp[(size_t)t0 * W + i];
+    __syncthreads();
+    Q2 n0 = rs[a], n1 = nc > 1 ? rs[W + a] : Q2{1.0, 0.0};
+    for (int t = 0; t < nc; ++t) {
+      const Q2 cs = n0;
+      n0 = n1;
+      if (t + 2 < nc) n1 = rs[(t + 2) * W + a];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const double x = qx[i], y = qy[i];
+        qx[i] = cs.x * x - cs.y * y;
+        qy[i] = bip_shift<W>(cs.y * x + cs.x * y, a);
+      }
+    }
+    __syncthreads();  // the next chunk overwrites rs
+  }
+  T* qo = Qall + (size_t)pair * N * N;
+  const int yc = W + (a + ns) % W;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    qo[(k0 + i) * N + a] = (T)qx[i];
+    qo[(k0 + i) * N + yc] = (T)qy[i];
+  }
+}
+
 // ------------------------------------------------------------------ apply
 // Q fragments are read kQPD k-steps ahead of their MFMA (row-layout Q).
 constexpr int kQPD = 8;
@@ -1305,13 +1635,17 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   return g;
 }
 
+static size_t rup256(size_t b) { return (b + 255) / 256 * 256; }
 static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   Geometry g = make_geometry(W, P, m_pad, 0);
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
-  // slabs + double-buffered Q and skip flags (evd(s+1) may run while apply(s) reads)
-  return ((slabs + 255) / 256 * 256) + 2 * ((q + 255) / 256 * 256) + 2 * ((sk + 255) / 256 * 256);
+  size_t rec = (size_t)P * kCrossMaxInner * W * W * sizeof(Pair2<double>);
+  // slabs + double-buffered Q and skip flags (evd(s+1) may run while apply(s)
+  // reads) + the cross EVD's rotation records and step counts (consumed by
+  // qbuild(s) before evd(s+1) on the same stream: single-buffered)
+  return rup256(slabs) + 2 * rup256(q) + 2 * rup256(sk) + rup256(rec) + rup256(sk);
 }
 
 // One chain of steps: resident buffers, its pair list and its workspace.
@@ -1325,6 +1659,8 @@ struct Chain {
   T* slabs;
   T* Qb[2];
   int32_t* skipb[2];
+  Pair2<double>* rec;  // cross EVD rotation records
+  int32_t* nsteps;
   hipStream_t st;
 };
 
@@ -1354,6 +1690,10 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   const size_t kstride = ((size_t)P * sizeof(int32_t) + 255) / 256 * 256;
   c.skipb[0] = (int32_t*)w;
   c.skipb[1] = (int32_t*)(w + kstride);
+  w += 2 * kstride;
+  c.rec = (Pair2<double>*)w;
+  w += rup256((size_t)P * kCrossMaxInner * W * W * sizeof(Pair2<double>));
+  c.nsteps = (int32_t*)w;
   return 0;
 }
 
@@ -1364,7 +1704,9 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                            uint32_t* metric) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
-  const int mode = c.modes ? c.modes[s] : 0;  // 0 cross, 1 full Gram, 2 cross + bipartite EVD
+  // 0 cross (cyclic EVD), 1 full Gram, 2 cross + bipartite EVD, 3 cross +
+  // cross-only bipartite EVD (evd_cross_kernel)
+  const int mode = c.modes ? c.modes[s] : 0;
   const int full = mode == 1;
   constexpr int XS = gram_xsplit<T, W>();
   if (full) {
@@ -1379,7 +1721,19 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   }
   SVDJ_LAUNCH_CHECK();
-  if (mode == 2)
+  if (mode == 3) {
+    hipLaunchKernelGGL((evd_cross_kernel<T, W>), dim3(c.P), dim3(cross_threads<W>()), 0, c.st, pr,
+                       c.slabs, c.g.gchunks, c.D, c.rec, c.nsteps, c.skipb[b], (T)tol, absmode,
+                       max_inner, metric);
+    SVDJ_LAUNCH_CHECK();
+    constexpr int RL = W == 64 ? 16 : 8;  // one workgroup per pair
+    if (c.P >= 32)
+      hipLaunchKernelGGL((qbuild_kernel<T, W, RL>), dim3(c.P, qbuild_blocks<W, RL>()),
+                         dim3(kQbThreads), 0, c.st, c.rec, c.nsteps, c.skipb[b], c.Qb[b]);
+    else
+      hipLaunchKernelGGL((qbuild_kernel<T, W, 4>), dim3(c.P, qbuild_blocks<W, 4>()),
+                         dim3(kQbThreads), 0, c.st, c.rec, c.nsteps, c.skipb[b], c.Qb[b]);
+  } else if (mode == 2)
     hipLaunchKernelGGL((evd_kernel<T, W, EVD_BIP>), dim3(c.P), dim3(evd_threads(W)), 0, c.st, pr,
                        0, c.slabs, c.g.gchunks, c.D, c.Qb[b], c.skipb[b], (T)tol, absmode,
                        max_inner, metric);
@@ -1517,6 +1871,14 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
 
 using namespace svdj;
 
+// Cross-step EVD ordering for a step of `pairs` pairs of W-wide blocks
+// (models/block.py choose_inner_order, measurements there): 2 = cross-only
+// (low-latency EVD + row-parallel Q build) for few W = 64 pairs, else 1 =
+// bipartite.  The inner_order codes of svdj_block_solve / svdj_dist_problem.
+extern "C" int svdj_choose_inner_order(int W, int pairs) {
+  return (W == 64 && pairs <= 16) ? 2 : 1;
+}
+
 extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
   return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);
 }
@@ -1632,11 +1994,12 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
       o[2 * k + 1] = a < b ? b : a;
     }
   }
-  if (inner_order < 0 || inner_order > 1) {
-    set_error("inner_order %d (0 cyclic, 1 bipartite)", inner_order);
+  if (inner_order == 3) inner_order = svdj_choose_inner_order(W, P);  // auto
+  if (inner_order < 0 || inner_order > 2) {
+    set_error("inner_order %d (0 cyclic, 1 bipartite, 2 cross, 3 auto)", inner_order);
     return -2;
   }
-  std::vector<int32_t> modes(steps, inner_order ? 2 : 0);
+  std::vector<int32_t> modes(steps, inner_order == 2 ? 3 : (inner_order ? 2 : 0));
   modes[0] = 1;
   hipStream_t st = (hipStream_t)stream;
   int32_t* dpairs = nullptr;

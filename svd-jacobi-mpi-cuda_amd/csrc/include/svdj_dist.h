@@ -62,7 +62,9 @@ typedef struct {
   int tol_mode;               // 0 relative, 1 absolute
   int max_sweeps;
   int mma;                    // matrix-core mode of the apply (svdj_block_steps)
-  int inner_order;            // EVD of the cross steps: 0 cyclic, 1 bipartite (mode 2)
+  int inner_order;            // EVD of the cross steps: 0 cyclic, 1 bipartite (mode 2),
+                              // 2 cross-only bipartite (mode 3), 3 auto
+                              // (svdj_choose_inner_order of the half super-block pairs)
   int stagger;                // 1: the two chains of a group offset by an EVD
                               // (svdj_block_steps2); 0 (default): issued independently
   void* stream_a;             // two compute streams (distinct)

@@ -59,7 +59,8 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 // D (device, dtype, [ncols]) holds squared column norms; updated in place.
 //   pairs   device int32 [steps][P][2] block indices
 //   modes   host   int32 [steps] (0 cross / 1 full / 2 cross with the bipartite
-//           EVD ordering, W steps instead of 2W-1), NULL = all cross
+//           EVD ordering, W steps instead of 2W-1 / 3 cross with the
+//           cross-only bipartite EVD), NULL = all cross
 //   metric  device uint32[2] as for the scalar path.
 //   tol_mode 0: rotate when |g_pq| > tol sqrt(g_pp g_qq) (relative, default);
 //            1: when |g_pq| > tol (the reference's absolute TOLERANCE test).
@@ -68,6 +69,9 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
 // Workspace size for one step: svdj_block_workspace_bytes().
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
+// inner_order code (1 bipartite, 2 cross-only) for steps of `pairs` pairs of
+// W-wide blocks: models/block.py choose_inner_order.
+int svdj_choose_inner_order(int W, int pairs);
 int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, const int32_t* pairs, int P,
                      int steps, const int32_t* modes, double tol, int tol_mode,
@@ -89,8 +93,8 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
 
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
-// step, 1 = bipartite EVD in the cross steps (mode 2).  Returns sweeps, <0 on
-// error.
+// step, 1 = bipartite EVD in the cross steps (mode 2), 2 = cross-only
+// bipartite EVD (mode 3).  Returns sweeps, <0 on error.
 int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, int ncols, double tol, int tol_mode,
                      int max_inner_sweeps, int max_sweeps, int inner_order, void* workspace,

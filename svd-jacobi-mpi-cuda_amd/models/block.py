@@ -37,6 +37,26 @@ def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     return 64 if (m >= 8192 and n >= 2048) else 32
 
 
+def choose_inner_order(W: int, pairs_per_step: int) -> str:
+    """EVD ordering of the cross steps for ``pairs_per_step`` pairs of W-wide
+    blocks per step (config inner_order="auto").
+
+    "cross" (evd_cross_kernel + qbuild_kernel: a low-latency EVD that
+    tracks only the cross couplings, Q built row-parallel by a second kernel)
+    when a step has few W=64 pairs and the EVD latency is on the critical
+    path; "bipartite" (one workgroup per pair, Q in registers) otherwise,
+    where the EVD hides under the other chain and its total CU time counts.
+    Measured on MI355X, 16384^2 fp32 rank plans, ms per sweep
+    bipartite / cross: P=8 (8 pairs) 59.1 / 51.0, P=4 (16) 112.5 / 108.1,
+    P=2 (32) 201.5 / 202.4; 1 GPU (64 pairs) 5.78 / 5.87 s per solve;
+    8192^2 P=8 (W=32) 20.0 / 22.1 (profiles/r3_evd)."""
+    return "cross" if (W == 64 and pairs_per_step <= 16) else "bipartite"
+
+
+def resolve_inner_order(order: str, W: int, pairs_per_step: int) -> str:
+    return choose_inner_order(W, pairs_per_step) if order == "auto" else order
+
+
 class BlockJacobi(Solver):
     name = "block"
 
@@ -62,9 +82,10 @@ class BlockJacobi(Solver):
         tol = self.tolerance(cfg.precision_dtype(A), m)
         with Timer(device) as tm:
             D = K.col_norms2(At, m_pad)
+            inner = resolve_inner_order(cfg.inner_order, W, ncols // (2 * W))
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
                                          cfg.max_sweeps, mma=mma, tol_mode=cfg.tol_mode,
-                                         inner_order=cfg.inner_order)
+                                         inner_order=inner)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:n, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:n, :n].t() if want_v else None

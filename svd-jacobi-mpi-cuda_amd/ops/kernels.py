@@ -214,17 +214,19 @@ def block_workspace(dtype, W, P, m_pad, device, slot: int = 0, pool: dict | None
     return ws
 
 
-INNER_ORDERS = ("cyclic", "bipartite")
+INNER_ORDERS = ("cyclic", "bipartite", "cross")
 
 
 def step_modes(modes, inner_order="cyclic"):
     """Plan modes (0 cross, 1 full) -> kernel modes: with the bipartite inner
     ordering cross steps become mode 2 (block.hip EVD_BIP, W EVD steps instead
-    of 2W-1); full steps always use the cyclic EVD."""
+    of 2W-1), with the cross-only ordering mode 3 (evd_cross_kernel: the
+    bipartite steps tracking only the cross couplings); full steps always use
+    the cyclic EVD."""
     if inner_order not in INNER_ORDERS:
         raise ValueError(f"inner_order must be one of {INNER_ORDERS}, got {inner_order!r}")
-    bip = inner_order == "bipartite"
-    return [2 if (bip and int(x) == 0) else int(x) for x in modes]
+    cm = {"cyclic": 0, "bipartite": 2, "cross": 3}[inner_order]  # "auto": resolve first
+    return [cm if int(x) == 0 else int(x) for x in modes]
 
 
 def check_block(dtype, W):
@@ -260,7 +262,7 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
         for s in range(steps):
             mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
                                       max_inner, tol_mode=tol_mode_code(tol_mode),
-                                      order="bipartite" if modes[s] == 2 else "cyclic")
+                                      order={2: "bipartite", 3: "cross"}.get(modes[s], "cyclic"))
             metric[0] = max(float(metric[0]), mx)
             metric[1] += nrot
 

@@ -88,20 +88,29 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
     """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
 
     Same orderings (``cyclic``: circle-method round robin over all pairs;
-    ``bipartite``: the cross pairs only), threshold and update formulas as
-    the LDS kernel (csrc/hip/block.hip evd_kernel).  Returns (G_diag_final,
-    Q, rotated).
+    ``bipartite``: the cross pairs only; ``cross``: the bipartite steps with
+    the within-block couplings held at zero, i.e. only the cross couplings
+    and the diagonal tracked -- block.hip evd_cross_kernel), threshold and
+    update formulas as the kernels.  Returns (G_diag_final, Q, rotated).
     """
     G = G.clone()
     P, N, _ = G.shape
     Q = torch.eye(N, dtype=G.dtype).expand(P, N, N).clone()
-    key = (N, order)
+    key = (N, "cyclic" if order == "cyclic" else "bipartite")
     sched = _RR_CACHE.get(key)
     if sched is None:
         prs_all = round_robin_pairs(N) if order == "cyclic" else bipartite_pairs(N // 2)
         sched = [(torch.tensor([a for a, b in prs]), torch.tensor([b for a, b in prs]))
                  for prs in prs_all]
         _RR_CACHE[key] = sched
+    within = None
+    if order == "cross":  # within-block couplings are never tracked
+        W = N // 2
+        within = torch.ones(N, N, dtype=torch.bool)
+        within[:W, W:] = False
+        within[W:, :W] = False
+        within.fill_diagonal_(False)
+        G[:, within] = 0
     rotated = torch.zeros(P, dtype=torch.bool)
     for _ in range(max_sweeps):
         sweep_rot = torch.zeros(P, dtype=torch.bool)
@@ -127,6 +136,8 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
             G[:, q, q] = gqq + t * gpq
             G[:, p, q] = torch.where(rot, torch.zeros_like(gpq), G[:, p, q])
             G[:, q, p] = G[:, p, q]
+            if within is not None:
+                G[:, within] = 0
             Qp, Qq = Q[:, :, p].clone(), Q[:, :, q].clone()
             Q[:, :, p] = c[:, None, :] * Qp - s[:, None, :] * Qq
             Q[:, :, q] = s[:, None, :] * Qp + c[:, None, :] * Qq

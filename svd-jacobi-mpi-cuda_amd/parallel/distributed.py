@@ -35,7 +35,7 @@ import torch
 from ..config import SolverConfig, SVDOptions
 from ..models.base import SVDResult, Solver
 from ..models import precondition as pre
-from ..models.block import choose_block
+from ..models.block import choose_block, resolve_inner_order
 from ..ops import kernels as K
 from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
@@ -257,6 +257,8 @@ class DistributedBlockJacobi(Solver):
                 K.set_identity(Vt[s * B:(s + 1) * B], B, held[s] * B)
         D = K.col_norms2(At, m_pad)
         tol = self.tolerance(pdtype, m)
+        # pairs per cross step: half super-blocks (pipelined) or whole ones
+        inner = resolve_inner_order(cfg.inner_order, W, k // 2 if pipelined else k)
         if pipelined:
             rA = rV = rD = None
         else:  # blocking exchange (chains=1) receives into a staging block
@@ -294,12 +296,12 @@ class DistributedBlockJacobi(Solver):
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                              inner_order=cfg.inner_order)
+                              inner_order=inner)
 
             def run_pair(a, b):
                 K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
                                mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                               inner_order=cfg.inner_order)
+                               inner_order=inner)
 
             if not cfg.stagger:
                 run_pair = None
@@ -319,7 +321,7 @@ class DistributedBlockJacobi(Solver):
                     with trace_range(f"svdj.round{r}"):
                         K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
                                       cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
-                                      tol_mode=cfg.tol_mode, inner_order=cfg.inner_order)
+                                      tol_mode=cfg.tol_mode, inner_order=inner)
                 mx, nrot = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
@@ -349,6 +351,7 @@ class DistributedBlockJacobi(Solver):
         sync()
         t_total = time.perf_counter() - t0
         info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
+                "inner_order": inner,
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
         if pipelined and P > 1:
             info["comm"] = ex.comm_summary()

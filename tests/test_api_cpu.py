@@ -141,3 +141,16 @@ def test_block_inner_order_cpu(order):
     assert rep["residual_rel"] < 1e-12 and rep["orth_v_fro"] < 1e-11, rep
     with pytest.raises(ValueError):
         svdj.svd(A, method="block", inner_order="sideways")
+
+
+@pytest.mark.parametrize("order", ["bipartite", "cross"])
+def test_block_cpu_inner_orders_converge(svdj, order):
+    """CPU oracle path of the block solver with the bipartite and cross-only
+    cross-step EVDs (ops/reference.py jacobi_evd): converged, fp64-accurate."""
+    import torch
+    A = svdj.utils.inputs.random_dense(200, 160, dtype=torch.float64, seed=4)
+    res = svdj.svd(A, method="block", block=32, inner_order=order)
+    assert res.converged, res.history
+    rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
+    assert rep["residual_rel"] < 1e-12 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
+    assert rep["orth_u_fro"] < 1e-10 and rep["orth_v_fro"] < 1e-10, rep

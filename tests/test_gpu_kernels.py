@@ -272,13 +272,17 @@ def test_fp64_block_widths_end_to_end(svdj, cuda, W):
     assert rep["orth_u_fro"] < 5e-11 and rep["orth_v_fro"] < 5e-11, rep
 
 
+@pytest.mark.parametrize("order,inner", [("bipartite", 1), ("cross", 1), ("cross", 3)])
 @pytest.mark.parametrize("dtype,W", [(torch.float32, 32), (torch.float32, 64),
                                      (torch.float64, 32), (torch.float64, 64)])
-def test_block_step_bipartite_matches_reference(svdj, cuda, dtype, W):
+def test_block_step_bipartite_matches_reference(svdj, cuda, dtype, W, order, inner):
     """Cross step with the bipartite EVD ordering (mode 2, block.hip
     Ord<W, EVD_BIP>: W steps of the cross pairs, DPP rotate + permlane32 swap
-    of the register Q) against the fp64 reference with the same ordering:
-    same rotation count, D and rotated panels to rounding level."""
+    of the register Q) or the cross-only one (mode 3, evd_cross_kernel: the
+    same steps tracking only the cross couplings, transpose-pair updates in
+    position space) against the fp64 reference with the same ordering, one or
+    several inner sweeps: same rotation count, D and rotated panels to
+    rounding level."""
     K = svdj.ops.kernels
     R = svdj.ops.reference
     nb = 4
@@ -295,26 +299,27 @@ def test_block_step_bipartite_matches_reference(svdj, cuda, dtype, W):
     At64, Vt64, D64 = At.double().cpu(), Vt.double().cpu(), D.double().cpu()
     tol = 1e-6 if dtype == torch.float32 else 1e-13
     metric = K.new_metric(cuda)
-    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [0], tol, 1, metric,
-                  inner_order="bipartite")
-    mx_ref, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, False, tol, 1,
-                                    order="bipartite")
+    K.block_steps(At, Vt, D, m_pad, pairs.to(cuda), W, [0], tol, inner, metric,
+                  inner_order=order)
+    mx_ref, nrot_ref = R.block_step(At64, Vt64, D64, pairs[0], W, False, tol, inner,
+                                    order=order)
     mx, nrot = K.read_metric(metric)
     assert nrot == nrot_ref == 2
     assert math.isclose(mx, mx_ref, rel_tol=1e-3)
-    rt = 3e-5 if dtype == torch.float32 else 1e-11
+    rt = (3e-5 if dtype == torch.float32 else 1e-11) * (1 if inner == 1 else 4)
     torch.testing.assert_close(At.double().cpu()[:, :m], At64[:, :m], rtol=rt, atol=rt)
     torch.testing.assert_close(Vt.double().cpu()[:, :n], Vt64[:, :n], rtol=rt, atol=rt)
     torch.testing.assert_close(D.double().cpu(), D64, rtol=rt, atol=rt)
 
 
+@pytest.mark.parametrize("order", ["bipartite", "cross"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-def test_svd_end_to_end_bipartite(svdj, cuda, dtype):
-    """Whole solve with bipartite cross steps: same accuracy bounds as the
-    cyclic inner ordering."""
+def test_svd_end_to_end_bipartite(svdj, cuda, dtype, order):
+    """Whole solve with bipartite / cross-only cross steps: same accuracy
+    bounds as the cyclic inner ordering."""
     m, n = 520, 384
     A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=3)
-    res = svdj.svd(A.to(cuda), method="block", dtype=dtype, inner_order="bipartite")
+    res = svdj.svd(A.to(cuda), method="block", dtype=dtype, inner_order=order)
     assert res.converged, res.history
     rep = svdj.utils.metrics.verify(A.to(cuda), res.U, res.S, res.V, torch.linalg.svdvals(A))
     r, sg, ou, ov = _E2E_BOUNDS[("block", dtype, "native")]

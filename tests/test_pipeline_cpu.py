@@ -200,3 +200,15 @@ def test_exposed_time_counts_each_moment_once():
     assert ex([(0, 10)], [(-5, 20)]) == 0              # fully hidden
     assert ex([(0, 3), (5, 8)], [(2, 6)]) == 4
     assert ex([], [(0, 1)]) == 0
+
+
+def test_native_inner_order_rule_matches_python():
+    """inner_order="auto": the native drivers (svdj_choose_inner_order in
+    libsvdj_hip) pick the cross-step EVD by the same rule as
+    models.block.choose_inner_order."""
+    choose = svdj.models.block.choose_inner_order
+    lib = svdj.ops.hip_lib()
+    code = {1: "bipartite", 2: "cross"}
+    for W in (32, 64):
+        for pairs in (1, 4, 8, 16, 17, 32, 64, 128, 256):
+            assert code[lib.svdj_choose_inner_order(W, pairs)] == choose(W, pairs), (W, pairs)

@@ -1,0 +1,81 @@
+// EVD kernel micro-benchmark (development aid): times one cross-step EVD
+// launch of P pairs (the block step's middle kernel) in isolation, for the
+// bipartite LDS kernel (mode 2) and the cross-only kernel (mode 3).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I<csrc/include> -I<csrc/hip> \
+//         tools/micro/evd_bench.hip -o evd_bench
+//   ./evd_bench P nchunk reps      (prints microseconds per launch)
+#include "block.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+void svdj::set_error(const char* fmt, ...) { (void)fmt; }
+
+template <typename K>
+static double time_it(K launch, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  launch();
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(a, nullptr);
+  for (int r = 0; r < reps; ++r) launch();
+  (void)hipEventRecord(b, nullptr);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms * 1e3 / reps;
+}
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 8, nchunk = argc > 2 ? atoi(argv[2]) : 1;
+  const int reps = argc > 3 ? atoi(argv[3]) : 50;
+  constexpr int W = 64;
+  std::vector<int32_t> hp(2 * P);
+  for (int p = 0; p < P; ++p) hp[2 * p] = 2 * p, hp[2 * p + 1] = 2 * p + 1;
+  std::vector<float> hs((size_t)P * nchunk * W * W), hd((size_t)2 * P * W);
+  unsigned s = 12345;
+  auto rnd = [&]() { s = s * 1664525u + 1013904223u; return (s >> 8) * (1.0f / 16777216.0f); };
+  for (auto& x : hs) x = (rnd() - 0.5f) * 0.2f / nchunk;
+  for (auto& x : hd) x = 1.0f + rnd();
+  int32_t *dp, *dsk, *dns;
+  float *dsl, *dD, *dQ;
+  uint32_t* dm;
+  svdj::Pair2<double>* drec;
+  (void)hipMalloc(&drec, (size_t)P * svdj::kCrossMaxInner * W * W * sizeof(*drec));
+  (void)hipMalloc(&dns, P * 4);
+  (void)hipMalloc(&dp, hp.size() * 4);
+  (void)hipMalloc(&dsl, hs.size() * 4);
+  (void)hipMalloc(&dD, hd.size() * 4);
+  (void)hipMalloc(&dQ, (size_t)P * 4 * W * W * 4);
+  (void)hipMalloc(&dsk, P * 4);
+  (void)hipMalloc(&dm, 8);
+  (void)hipMemcpy(dp, hp.data(), hp.size() * 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dsl, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+  auto reset = [&]() { (void)hipMemcpy(dD, hd.data(), hd.size() * 4, hipMemcpyHostToDevice); };
+  reset();
+  const double tb = time_it([&]() {
+    hipLaunchKernelGGL((svdj::evd_kernel<float, W, svdj::EVD_BIP>), dim3(P), dim3(svdj::evd_threads(W)), 0,
+                       nullptr, dp, 0, dsl, nchunk, dD, dQ, dsk, 1e-6f, 0, 1, dm);
+  }, reps);
+  reset();
+  const double tc = time_it([&]() {
+    hipLaunchKernelGGL((svdj::evd_cross_kernel<float, W>), dim3(P), dim3(svdj::cross_threads<W>()), 0,
+                       nullptr, dp, dsl, nchunk, dD, drec, dns, dsk, 1e-6f, 0, 1, dm);
+  }, reps);
+  reset();
+  const double tq = time_it([&]() {
+    hipLaunchKernelGGL((svdj::evd_cross_kernel<float, W>), dim3(P), dim3(svdj::cross_threads<W>()), 0,
+                       nullptr, dp, dsl, nchunk, dD, drec, dns, dsk, 1e-6f, 0, 1, dm);
+    if (P >= 32)
+      hipLaunchKernelGGL((svdj::qbuild_kernel<float, W, 16>), dim3(P, svdj::qbuild_blocks<W, 16>()),
+                         dim3(svdj::kQbThreads), 0, nullptr, drec, dns, dsk, dQ);
+    else
+      hipLaunchKernelGGL((svdj::qbuild_kernel<float, W, 4>), dim3(P, svdj::qbuild_blocks<W, 4>()),
+                         dim3(svdj::kQbThreads), 0, nullptr, drec, dns, dsk, dQ);
+  }, reps);
+  std::printf("P %d nchunk %d: bipartite %.2f us  cross evd %.2f us  cross evd+qbuild %.2f us\n",
+              P, nchunk, tb, tc, tq);
+  return 0;
+}
