@@ -551,7 +551,7 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
   for (int c = 0; c < 2 && !rc; ++c)
     if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);
-  if (!rc && hipMalloc((void**)&h->metric, 2 * sizeof(uint32_t)) != hipSuccess)
+  if (!rc && hipMalloc((void**)&h->metric, 4 * sizeof(uint32_t)) != hipSuccess)
     rc = fail(-100, "hipMalloc(metric) failed");
   if (!rc && !h->sc && h->world > 1) {
     if (hipStreamCreateWithFlags(&h->sc, hipStreamNonBlocking) != hipSuccess)
@@ -818,6 +818,9 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   int rc = 0;
   p->sweeps = 0;
   p->converged = 0;
+  // underflow floor of the block EVDs (block.hip needs_rotation)
+  if (svdj_set_norm_floor(svdj_norm_floor_value(h->dtype, h->m_pad), h->metric, sa) < 0)
+    return fail(-100, "norm floor: %s", svdj_hip_last_error());
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;
     // ---- stop test: global max convergence value (positive floats order as

@@ -292,17 +292,34 @@ __device__ __forceinline__ double dpp_shl1(double v) {
 // two decide identically: relative |g_pq| > tol sqrt(g_pp g_qq) (fp32: raw
 // v_sqrt, ~1 ulp), or the reference's absolute |g_pq| > tol (TOLERANCE,
 // reference lib/global.cuh:9, main.cu:714) when absmode.
+//
+// Underflowing columns: in the relative mode a pair is rotated only if both
+// squared norms exceed `floor` = m realmin / eps (metric[2..3], set once per
+// solve, svdj_set_norm_floor).  Below it the squared norms and dot products
+// of a column lose their precision to underflow (the entries' products
+// approach realmin), so the relative coupling is noise and the pair would be
+// rotated forever.  LAPACK's xGESVJ likewise skips columns below its safe
+// minimum.  The reference's own input (upper-triangular U(0,1)) has
+// sigma_min / sigma_max ~ 2^-n: at n = 5000 most columns end far below
+// fp64's range, and without the floor the solve did not converge in 60
+// sweeps (profiles/r3_refshape); columns above it keep one-sided Jacobi's
+// relative accuracy (n = 300: U orthogonal to 1e-12).  0 = off.
 __device__ __forceinline__ bool needs_rotation(float gpp, float gqq, float gpq, float tol,
-                                               int absmode) {
+                                               int absmode, float floor = 0.0f) {
   if (absmode) return fabsf(gpq) > tol;
   const float nrm = __builtin_amdgcn_sqrtf(gpp) * __builtin_amdgcn_sqrtf(gqq);
-  return nrm > 0.0f && fabsf(gpq) > tol * nrm;
+  return nrm > 0.0f && fabsf(gpq) > tol * nrm && fminf(gpp, gqq) > floor;
 }
 __device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gpq, double tol,
-                                               int absmode) {
+                                               int absmode, double floor = 0.0) {
   if (absmode) return fabs(gpq) > tol;
   const double nrm = sqrt(gpp) * sqrt(gqq);
-  return nrm > 0.0 && fabs(gpq) > tol * nrm;
+  return nrm > 0.0 && fabs(gpq) > tol * nrm && fmin(gpp, gqq) > floor;
+}
+// The negligible-column floor of this solve (metric[2..3], a double).
+template <typename T>
+__device__ __forceinline__ T norm_floor(const uint32_t* metric) {
+  return (T)*reinterpret_cast<const double*>(metric + 2);
 }
 
 // Rotation of one slot, branch-free (the solve sits on the EVD's critical
@@ -310,8 +327,9 @@ __device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gp
 // test fails.  fp32: raw v_sqrt/v_rcp/v_rsq (~1 ulp) -- (c, s) only steer G;
 // the fp64 Q is built from t.
 __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, float tol,
-                                              int absmode, float& c, float& s, float& t) {
-  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode);
+                                              int absmode, float floor, float& c, float& s,
+                                              float& t) {
+  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode, floor);
   const float g = rot ? gpq : 1.0f;
   const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * g);
   const float at = fabsf(tau);
@@ -324,8 +342,9 @@ __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, f
   return rot;
 }
 __device__ __forceinline__ bool rotation_fast(double gpp, double gqq, double gpq, double tol,
-                                              int absmode, double& c, double& s, double& t) {
-  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode);
+                                              int absmode, double floor, double& c, double& s,
+                                              double& t) {
+  const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode, floor);
   const double g = rot ? gpq : 1.0;
   const double tau = (gqq - gpp) / (2.0 * g);
   const double at = fabs(tau);
@@ -657,6 +676,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T nfloor = norm_floor<T>(metric);
 
   // ---- assemble G: diagonal first (player order), then every off-diagonal
   // entry into position space for step 0; split-K slabs summed in fp64
@@ -680,11 +700,11 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       Gb[0][tri_idx<N>(O::pos0(r), O::pos0(c))] = g;
       const T grr = dg[r], gcc = dg[c];
       const T d = sqrt(grr) * sqrt(gcc);
-      if (d > T(0)) {
+      if (d > T(0) && (absmode || (grr > nfloor && gcc > nfloor))) {
         const float v = (float)(fabs(g) / d);
         mx = v > mx ? v : mx;
       }
-      need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
+      need |= needs_rotation(grr, gcc, g, tol, absmode, nfloor) ? 1 : 0;
     };
     // Slab sums with 16-byte loads, all chunks of a group in flight at once
     // (one dependent global load per entry and chunk was ~12 us per kernel).
@@ -825,7 +845,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     const T gpp = dg[p], gqq = dg[q];
     const T gpq = Gb[0][tri_idx<N>(fa, sa)];
     T c, s, t;
-    const bool rot = rotation_fast(gpp, gqq, gpq, tol, absmode, c, s, t);
+    const bool rot = rotation_fast(gpp, gqq, gpq, tol, absmode, nfloor, c, s, t);
     racc = rot;
     // thread tid's duty block holds next-step slot tid (EvdDeal), so phase 0's
     // pending write moves this coupling to its step-1 position
@@ -880,7 +900,7 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
       const T g = e == 0 ? h[0] : e == 1 ? h[1] : e == 2 ? h[2] : h[3];
       const T df = x_first ? k.dx : k.dy, ds = x_first ? k.dy : k.dx;
       T c, sn, t;
-      const bool rot = rotation_fast(df, ds, g, tol, absmode, c, sn, t);
+      const bool rot = rotation_fast(df, ds, g, tol, absmode, nfloor, c, sn, t);
       if (last) racc_next |= rot; else racc |= rot;
       pend = rot ? T(0) : g;
       publish(nb, ns, c, sn, t, df - t * g, ds + t * g);
@@ -1040,6 +1060,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
   const int pair = blockIdx.x;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T nfloor = norm_floor<T>(metric);
 
   // ---- assemble: diagonals from D, E_0[i][p] = C[i][p] (split-K slabs
   // summed in fp64), convergence value and the "anything to rotate" test
@@ -1068,11 +1089,11 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
         Eb[0][i] = g;
         const T grr = dg[i / W], gcc = dg[W + i % W];
         const T d = sqrt(grr) * sqrt(gcc);
-        if (d > T(0)) {
+        if (d > T(0) && (absmode || (grr > nfloor && gcc > nfloor))) {
           const float v = (float)(fabs(g) / d);
           mx = v > mx ? v : mx;
         }
-        need |= needs_rotation(grr, gcc, g, tol, absmode) ? 1 : 0;
+        need |= needs_rotation(grr, gcc, g, tol, absmode, nfloor) ? 1 : 0;
       }
     }
     mx = wave_max(mx);
@@ -1134,7 +1155,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
   Q2* rq = rec + (size_t)pair * (kCrossMaxInner * W) * W;
   auto solve = [&](T dx, T dy, T g, int step, bool& rot) {
     T c, sn, t;
-    rot = rotation_fast(dx, dy, g, tol, absmode, c, sn, t);
+    rot = rotation_fast(dx, dy, g, tol, absmode, nfloor, c, sn, t);
     double c64, s64;
     if constexpr (sizeof(T) == 8) {
       c64 = c;
@@ -2008,7 +2029,9 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
                                 hipMemcpyHostToDevice, st));
   int sweeps = 0, rc = 0;
   uint32_t hm[2];
-  for (int sw = 0; sw < max_sweeps; ++sw) {
+  // underflow floor of this solve (metric[2..3])
+  rc = svdj_set_norm_floor(svdj_norm_floor_value(dtype, m_pad), metric, stream);
+  for (int sw = 0; sw < max_sweeps && rc >= 0; ++sw) {
     if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
     rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,
                           modes.data(), tol, tol_mode, max_inner, ws, ws_bytes, metric, mma,

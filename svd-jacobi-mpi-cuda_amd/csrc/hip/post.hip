@@ -139,6 +139,23 @@ extern "C" int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int
   return 0;
 }
 
+// metric[2..3] (a double) = the underflow floor of the block EVDs
+// (block.hip needs_rotation): squared norms at or below m realmin / eps.
+__global__ void norm_floor_kernel(double v, uint32_t* __restrict__ metric) {
+  if (threadIdx.x == 0) *reinterpret_cast<double*>(metric + 2) = v;
+}
+
+extern "C" double svdj_norm_floor_value(int dtype, int m) {
+  return dtype == 1 ? (double)m * 2.2250738585072014e-308 / 2.220446049250313e-16
+                    : (double)m * 1.1754943508222875e-38 / 1.1920928955078125e-07;
+}
+
+extern "C" int svdj_set_norm_floor(double floor, uint32_t* metric, void* stream) {
+  hipLaunchKernelGGL(norm_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, floor, metric);
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma,
                              int scale_u, void* stream) {
   if (ncols <= 0) return 0;

@@ -61,7 +61,9 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   modes   host   int32 [steps] (0 cross / 1 full / 2 cross with the bipartite
 //           EVD ordering, W steps instead of 2W-1 / 3 cross with the
 //           cross-only bipartite EVD), NULL = all cross
-//   metric  device uint32[2] as for the scalar path.
+//   metric  device uint32[4]: [0] max convergence value (float bits), [1]
+//           rotated pairs, [2..3] the underflow floor (double,
+//           svdj_set_norm_floor; 0 = off).
 //   tol_mode 0: rotate when |g_pq| > tol sqrt(g_pp g_qq) (relative, default);
 //            1: when |g_pq| > tol (the reference's absolute TOLERANCE test).
 //   mma     matrix-core mode: 0 native (f32 / f64 MFMA), 1 fp32 data on bf16
@@ -116,6 +118,12 @@ int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld, const voi
 int svdj_set_identity(int dtype, void* V, int n_v, int ldv, int ncols, int col_offset, void* stream);
 // Squared column norms D[c] = sum_i A[i,c]^2 (fp64 accumulation).
 int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int ncols, void* D, void* stream);
+// The block EVDs' underflow floor (relative mode: pairs with a squared norm
+// <= it are not rotated): svdj_norm_floor_value = m realmin / eps of the
+// data type; svdj_set_norm_floor stores it at metric[2..3] (metric holds 4
+// uint32), once per solve.
+double svdj_norm_floor_value(int dtype, int m);
+int svdj_set_norm_floor(double floor, uint32_t* metric, void* stream);
 // sigma[c] = ||a_c||; if scale_u, a_c /= sigma[c] (sigma == 0 columns untouched).
 int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma, int scale_u, void* stream);
 

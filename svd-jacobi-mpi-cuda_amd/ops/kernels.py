@@ -78,13 +78,34 @@ def _check_layout(At: torch.Tensor, m_pad: int):
 
 # ------------------------------------------------------------------ metric
 def new_metric(device) -> torch.Tensor:
+    """Per-sweep stop-test state: [0] max convergence value, [1] rotated
+    pairs, and (block path) the negligible-column floor of the solve
+    (device: int32[4], the floor a double in [2..3]; CPU: float64[3])."""
     if torch.device(device).type == "cpu":
-        return torch.zeros(2, dtype=torch.float64)
-    return torch.zeros(2, dtype=torch.int32, device=device)
+        return torch.zeros(3, dtype=torch.float64)
+    return torch.zeros(4, dtype=torch.int32, device=device)
 
 
 def reset_metric(metric: torch.Tensor):
-    metric.zero_()
+    metric[:2].zero_()  # the floor (set once per solve) stays
+
+
+def norm_floor(dtype: torch.dtype, m: int) -> float:
+    """Underflow floor m realmin / eps of the working type: the block EVDs
+    (block.hip needs_rotation) do not rotate pairs with a squared column norm
+    at or below it -- its products and sums have lost their precision to
+    underflow (LAPACK xGESVJ skips such columns likewise)."""
+    fi = torch.finfo(torch.float64 if dtype == torch.float64 else torch.float32)
+    return m * fi.tiny / fi.eps
+
+
+def set_norm_floor(metric: torch.Tensor, dtype: torch.dtype, m: int):
+    """Store :func:`norm_floor` in the metric (once per solve)."""
+    v = norm_floor(dtype, m)
+    if metric.device.type == "cpu":
+        metric[2] = v
+    else:
+        metric[2:4].view(torch.float64).fill_(v)
 
 
 def read_metric(metric: torch.Tensor):
@@ -262,6 +283,7 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
         for s in range(steps):
             mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
                                       max_inner, tol_mode=tol_mode_code(tol_mode),
+                                      floor=float(metric[2]) if metric.numel() > 2 else 0.0,
                                       order={2: "bipartite", 3: "cross"}.get(modes[s], "cyclic"))
             metric[0] = max(float(metric[0]), mx)
             metric[1] += nrot
@@ -351,8 +373,10 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
     pairs = torch.from_numpy(round_robin(nb))
     modes = [1] + [0] * (nb - 2)
     hist = []
+    metric = new_metric("cpu")
+    set_norm_floor(metric, At.dtype, m_pad)
     for _ in range(max_sweeps):
-        metric = new_metric("cpu")
+        reset_metric(metric)
         block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric,
                     tol_mode=tol_mode, inner_order=inner_order)
         mx, nrot = read_metric(metric)
@@ -363,7 +387,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
 
 
 __all__ = [
-    "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric",
+    "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric", "set_norm_floor",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",

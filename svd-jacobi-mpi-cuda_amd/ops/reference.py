@@ -84,7 +84,7 @@ def bipartite_pairs(W):
     return [[(a, W + (a + t) % W) for a in range(W)] for t in range(W)]
 
 
-def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
+def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic", floor: float = 0.0):
     """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
 
     Same orderings (``cyclic``: circle-method round robin over all pairs;
@@ -117,7 +117,8 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
         for p, q in sched:
             gpp, gqq, gpq = G[:, p, p], G[:, q, q], G[:, p, q]
             nrm = gpp.clamp(min=0).sqrt() * gqq.clamp(min=0).sqrt()
-            rot = (gpq.abs() > tol) if tol_mode == 1 else (nrm > 0) & (gpq.abs() > tol * nrm)
+            rot = (gpq.abs() > tol) if tol_mode == 1 else (
+                (nrm > 0) & (gpq.abs() > tol * nrm) & (torch.minimum(gpp, gqq) > floor))
             if not bool(rot.any()):
                 continue
             sweep_rot |= rot.any(1)
@@ -148,7 +149,7 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic"):
 
 
 def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
-               order: str = "cyclic"):
+               order: str = "cyclic", floor: float = 0.0):
     """One block step on P disjoint block pairs (pairs: (P, 2) block ids).
 
     Mirrors csrc/hip/block.hip (gram -> evd -> apply).  Updates At, Vt, D in
@@ -179,9 +180,12 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
     dg = torch.diagonal(G, dim1=1, dim2=2).clamp(min=0).sqrt()
     den = dg[:, :, None] * dg[:, None, :]
     R = torch.where(den > 0, G.abs() / torch.where(den > 0, den, torch.ones_like(den)), torch.zeros_like(den))
+    if tol_mode != 1 and floor > 0:  # couplings of negligible columns do not count
+        big = torch.diagonal(G, dim1=1, dim2=2) > floor
+        R = torch.where(big[:, :, None] & big[:, None, :], R, torch.zeros_like(R))
     maxconv = float(R[:, mask].max()) if mask.any() else 0.0
     lam, Q, rotated = jacobi_evd(G, tol, max_inner, tol_mode,
-                                 order="cyclic" if full else order)
+                                 order="cyclic" if full else order, floor=floor)
     if bool(rotated.any()):
         sel = rotated
         Qs = Q[sel]

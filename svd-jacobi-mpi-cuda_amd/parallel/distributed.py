@@ -266,6 +266,7 @@ class DistributedBlockJacobi(Solver):
             rV = torch.empty(B, n_v, dtype=dtype, device=dev) if want_v else None
             rD = torch.empty(B, dtype=dtype, device=dev)
         metric = K.new_metric(dev)
+        K.set_norm_floor(metric, dtype, m_pad)
         comm.barrier()
 
         hist, t_comm, t_total = [], 0.0, 0.0

@@ -154,3 +154,38 @@ def test_block_cpu_inner_orders_converge(svdj, order):
     rep = svdj.utils.metrics.verify(A, res.U, res.S, res.V, torch.linalg.svdvals(A))
     assert rep["residual_rel"] < 1e-12 and rep["sigma_max_abs_err_over_smax"] < 1e-12, rep
     assert rep["orth_u_fro"] < 1e-10 and rep["orth_v_fro"] < 1e-10, rep
+
+
+def test_block_converges_on_reference_triangular_input(svdj):
+    """The reference's default input (upper-triangular U(0,1), numerically
+    singular: sigma_min / sigma_max ~ 2^-n) converges, with U and V
+    orthogonal: one-sided Jacobi keeps relative accuracy for the tiny
+    columns (the underflow floor, ops.kernels.norm_floor, only acts far
+    below them at this size)."""
+    import torch
+    A = svdj.utils.inputs.reference_triu(160)
+    res = svdj.svd(A, method="block", block=32, max_sweeps=40)
+    assert res.converged and res.sweeps < 40, res.history
+    V, U, S = res.V, res.U, res.S
+    assert (V.t() @ V - torch.eye(160, dtype=V.dtype)).norm() < 1e-10
+    assert (U.t() @ U - torch.eye(160, dtype=U.dtype)).norm() < 1e-8
+    assert (A @ V - U * S).norm() / A.norm() < 1e-12
+
+
+def test_norm_floor_skips_underflowing_columns(svdj):
+    """A pair whose column's squared norm is at or below the underflow floor
+    is not rotated (ops/reference.py mirrors block.hip needs_rotation)."""
+    import torch
+    K, R = svdj.ops.kernels, svdj.ops.reference
+    assert K.norm_floor(torch.float64, 1000) == 1000 * torch.finfo(torch.float64).tiny / \
+        torch.finfo(torch.float64).eps
+    G = torch.tensor([[[1.0, 0.5, 0.0, 0.0], [0.5, 1.0, 0.0, 0.0],
+                       [0.0, 0.0, 1e-300, 5e-301], [0.0, 0.0, 5e-301, 1e-300]]],
+                     dtype=torch.float64)
+    _, _, rot = R.jacobi_evd(G, 1e-14, 1, floor=K.norm_floor(torch.float64, 8))
+    assert bool(rot[0])                      # the (0, 1) pair rotates
+    G[0, 0, 1] = G[0, 1, 0] = 0.0
+    _, Q, rot = R.jacobi_evd(G, 1e-14, 1, floor=K.norm_floor(torch.float64, 8))
+    assert not bool(rot[0])                  # the underflowing (2, 3) pair does not
+    _, _, rot = R.jacobi_evd(G, 1e-14, 1, floor=0.0)
+    assert bool(rot[0])

@@ -92,3 +92,17 @@ def test_native_persistent_handle_repeat_solves():
     assert r.returncode == 0, out[-4000:]
     assert "converged: 1" in out and "exposed_comm_ms:" in out, out
     assert _value(out, "||A-USVt||_F/||A||_F:") < 2e-5, out
+
+
+def test_native_dist_reference_triangular_input_converges():
+    """The reference's own run (triangular U(0,1) input, fp64, 2 ranks --
+    build/runSVDMPICUDAWithoutCMake.slurm:30) converges: the negligible-
+    column floor keeps noise-level columns from being rotated forever."""
+    r = subprocess.run([_exe(), "1200", "--np", "2", "--shared-gpu", "--dtype", "f64",
+                        "--verify", "--timeout", "120"], capture_output=True, text=True,
+                       timeout=170)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "converged: 1" in out, out
+    assert _value(out, "||A-USVt||_F/||A||_F:") < 1e-12, out
+    assert _value(out, "||V^TV-I||_F:") < 1e-9, out
