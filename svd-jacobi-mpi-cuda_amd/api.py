@@ -56,7 +56,7 @@ def svd(A: torch.Tensor, jobu=SVDOptions.AllVec, jobv=SVDOptions.AllVec,
     Q = None
     if pre.use_qr(cfg, mm, nn):
         # tall-skinny: Jacobi on R (n x n), U = Q U_R (models/precondition.py)
-        Q, R = pre.qr(A.to(dev), cfg.resolved_dtype(A))
+        Q, R, Lt = pre.qr_deferred(A.to(dev), cfg.resolved_dtype(A))
         A = R.to(A.dtype) if cfg.bf16_mode(A) else R
     if method == "oracle":
         res = solver.solve(A, jobu, jobv)
@@ -64,7 +64,7 @@ def svd(A: torch.Tensor, jobu=SVDOptions.AllVec, jobv=SVDOptions.AllVec,
         res = solver.solve(A, jobu, jobv, device=dev)
     if Q is not None:
         if res.U is not None:
-            res.U = (Q.to(res.U.device) @ res.U.to(Q.dtype)).to(res.U.dtype)
+            res.U = pre.apply_q(Q, Lt, res.U.to(Q.device)).to(res.U.dtype)
         res.info["precondition"] = "qr"
     res.info["flops"] = pre.flops(mm, nn, res.sweeps, Q is not None)
     if transposed:

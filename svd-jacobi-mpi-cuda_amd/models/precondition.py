@@ -34,6 +34,19 @@ def qr(A: torch.Tensor, dtype: torch.dtype, method: str = "auto"):
     (rocSOLVER geqrf on the GPU, which made QR cost more than it saved at
     32768 x 8192).  ``auto``: CholeskyQR2 on the GPU, Householder if the Gram
     is not numerically positive definite (or on the CPU)."""
+    Q1, R, Lt = qr_deferred(A, dtype, method)
+    return (Q1, R) if Lt is None else (
+        torch.linalg.solve_triangular(Lt, Q1, upper=True, left=False), R)
+
+
+def qr_deferred(A: torch.Tensor, dtype: torch.dtype, method: str = "auto"):
+    """(Q1, R, Lt) with Q = Q1 Lt^-1 (Lt upper triangular n x n, or None when
+    Q1 is Q itself).  The solvers never form Q: they only need U = Q U_R =
+    Q1 (Lt^-1 U_R) (``apply_q``), so CholeskyQR2's second m x n TRSM becomes
+    an n x n one.  Measured on MI355X at 32768 x 8192 fp32
+    (tools/qr_breakdown.py, profiles/r3_fusion): the m x n TRSM is 17.5 ms,
+    the Gram GEMMs and the U GEMM run at 153 TFLOP/s (97 % of the fp32
+    matrix-core peak) in hipBLASLt, the two 8192 Choleskys take 28.8 ms each."""
     A = A.to(dtype)
     if method in ("auto", "cholqr2") and (A.is_cuda or method == "cholqr2"):
         out = _cholqr2(A)
@@ -42,56 +55,65 @@ def qr(A: torch.Tensor, dtype: torch.dtype, method: str = "auto"):
         if method == "cholqr2":
             raise RuntimeError("CholeskyQR2 failed: Gram not positive definite (ill-conditioned A)")
     Q, R = torch.linalg.qr(A, mode="reduced")
-    return Q, R
+    return Q, R, None
+
+
+def apply_q(Q1: torch.Tensor, Lt, X: torch.Tensor) -> torch.Tensor:
+    """Q X for Q = Q1 Lt^-1 (``qr_deferred`` / ``dist_qr``): one n x n
+    triangular solve, then the m x n x n GEMM."""
+    if Lt is not None:
+        X = torch.linalg.solve_triangular(Lt, X.to(Lt.dtype), upper=True)
+    return Q1 @ X.to(Q1.dtype)
 
 
 def _cholqr2(A: torch.Tensor):
-    """None when A is too ill-conditioned for CholeskyQR2 (kappa >~ eps^-1/2,
-    estimated from the first Cholesky factor's pivots)."""
+    """(Q1, R, L2^T), or None when A is too ill-conditioned for CholeskyQR2
+    (kappa >~ eps^-1/2, estimated from the first Cholesky factor's pivots)."""
     eps = torch.finfo(A.dtype).eps
-    Q, R = A, None
-    for it in range(2):
-        L, info = torch.linalg.cholesky_ex(Q.t() @ Q)
-        if int(info) != 0 or not bool(torch.isfinite(L).all()):
-            return None
-        if it == 0:
-            d = torch.diagonal(L).abs()
-            if float(d.min()) <= eps ** 0.5 * float(d.max()):
-                return None
-        Q = torch.linalg.solve_triangular(L.t(), Q, upper=True, left=False)  # Q L^-T
-        R = L.t() if R is None else L.t() @ R
-    return Q, R
+    L1, info = torch.linalg.cholesky_ex(A.t() @ A)
+    if int(info) != 0 or not bool(torch.isfinite(L1).all()):
+        return None
+    d = torch.diagonal(L1).abs()
+    if float(d.min()) <= eps ** 0.5 * float(d.max()):
+        return None
+    Q1 = torch.linalg.solve_triangular(L1.t(), A, upper=True, left=False)  # A L1^-T
+    L2, info = torch.linalg.cholesky_ex(Q1.t() @ Q1)
+    if int(info) != 0 or not bool(torch.isfinite(L2).all()):
+        return None
+    return Q1, L2.t() @ L1.t(), L2.t()
 
 
 def dist_qr(A_loc: torch.Tensor, dtype: torch.dtype, comm):
     """Row-distributed CholeskyQR2: rank g holds rows A_g (m_g x n) of A.
 
-    Twice: G = sum_g Q_g^T Q_g (local GEMM + one n x n all-reduce over
-    RCCL), G = L L^T (redundant on every rank: every rank sees the same G),
-    Q_g <- Q_g L^-T (local TRSM).  R = L2^T L1^T is replicated, so every rank
-    can take its super-blocks of R with no further communication, and Q stays
-    row-distributed (U = Q U_R is then a local GEMM per row block).  The QR
-    cost is divided by P; the replicated m x n factorisation it replaces
-    was redundant work on every rank.
+    G1 = sum_g A_g^T A_g (local GEMM + one n x n all-reduce over RCCL),
+    G1 = L1 L1^T (redundant on every rank: every rank sees the same G1),
+    Q1_g = A_g L1^-T (local TRSM), then G2 = sum_g Q1_g^T Q1_g = L2 L2^T the
+    same way.  R = L2^T L1^T is replicated, so every rank can take its
+    super-blocks of R with no further communication; Q = Q1 L2^-T stays
+    row-distributed and unformed (U = Q U_R is ``apply_q`` per row block).
+    The QR cost is divided by P; the replicated m x n factorisation it
+    replaces was redundant work on every rank.
 
-    Returns (Q_g, R), or None when the Gram is not numerically positive
+    Returns (Q1_g, R, L2^T), or None when a Gram is not numerically positive
     definite (kappa(A) >~ eps^-1/2) -- the same decision on every rank."""
-    Q = A_loc.to(dtype)
+    A = A_loc.to(dtype)
     eps = torch.finfo(dtype).eps
-    R = None
-    for it in range(2):
-        G = Q.t() @ Q
-        comm.allreduce_sum_(G)
-        L, info = torch.linalg.cholesky_ex(G)
-        if int(info) != 0 or not bool(torch.isfinite(L).all()):
-            return None
-        if it == 0:
-            d = torch.diagonal(L).abs()
-            if float(d.min()) <= eps ** 0.5 * float(d.max()):
-                return None
-        Q = torch.linalg.solve_triangular(L.t(), Q, upper=True, left=False)  # Q L^-T
-        R = L.t() if R is None else L.t() @ R
-    return Q, R
+    G = A.t() @ A
+    comm.allreduce_sum_(G)
+    L1, info = torch.linalg.cholesky_ex(G)
+    if int(info) != 0 or not bool(torch.isfinite(L1).all()):
+        return None
+    d = torch.diagonal(L1).abs()
+    if float(d.min()) <= eps ** 0.5 * float(d.max()):
+        return None
+    Q1 = torch.linalg.solve_triangular(L1.t(), A, upper=True, left=False)  # A L1^-T
+    G = Q1.t() @ Q1
+    comm.allreduce_sum_(G)
+    L2, info = torch.linalg.cholesky_ex(G)
+    if int(info) != 0 or not bool(torch.isfinite(L2).all()):
+        return None
+    return Q1, L2.t() @ L1.t(), L2.t()
 
 
 def flops(m: int, n: int, sweeps: int, qr_used: bool) -> float:

@@ -120,10 +120,10 @@ class DistributedBlockJacobi(Solver):
         out = pre.dist_qr(A_loc, work, comm)
         if out is None:  # too ill-conditioned for CholeskyQR2: replicated Householder
             Qf, R = pre.qr(self._allgather_rows(A_loc, m, n), work, method="householder")
-            Q_loc = Qf[r0:r1].contiguous()
+            Q_loc, Lt = Qf[r0:r1].contiguous(), None
             del Qf
         else:
-            Q_loc, R = out
+            Q_loc, R, Lt = out
         del A_loc
         if cfg.comm_timing and dev.type == "cuda":  # phase timing costs a sync
             torch.cuda.synchronize(dev)
@@ -132,7 +132,7 @@ class DistributedBlockJacobi(Solver):
                           time_only)
         want_u = jobu != SVDOptions.NoVec
         U_R, S, V = self._allgather_columns(res, n, want_u, jobv != SVDOptions.NoVec)
-        U_loc = (Q_loc @ U_R).to(U_R.dtype) if want_u else None
+        U_loc = pre.apply_q(Q_loc, Lt, U_R).to(U_R.dtype) if want_u else None
         res.S, res.V = S, V
         res.info.update(precondition="qr", flops=pre.flops(m, n, res.sweeps, True),
                         qr_seconds=round(t_qr, 4),
