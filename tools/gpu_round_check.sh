@@ -11,6 +11,9 @@ tail -3 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python bench.py --n $N --steps 1 --warmup 1 > gpurun_out/bench_$N.log 2>&1 \
   || { tail -20 gpurun_out/bench_$N.log; exit 1; }
 tail -1 gpurun_out/bench_$N.log
+timeout -k 10 200 python bench.py --m 32768 --n 8192 --steps 2 --warmup 1 > gpurun_out/bench_tall.log 2>&1 \
+  || { tail -20 gpurun_out/bench_tall.log; exit 1; }
+tail -1 gpurun_out/bench_tall.log | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$N -o run \
   --output-format csv -- python $R/bench.py --n $N --steps 1 --warmup 0 \
