@@ -207,7 +207,8 @@ def simulate(a, cfg, dtype, work):
             return made.pop(0).double().pow(2).sum(1).to(like.dtype)
         return torch.zeros_like(like)
 
-    comm = SimCommunicator(P, g, dev, seed_fn=seed, link_gbps=a.sim_link_gbps)
+    comm = SimCommunicator(P, g, dev, seed_fn=seed, link_gbps=a.sim_link_gbps,
+                           exchange=a.exchange)
     cfg.max_sweeps = a.sim_sweeps
     cfg.comm_timing = True
     solver = DistributedBlockJacobi(cfg, comm)
@@ -229,7 +230,7 @@ def simulate(a, cfg, dtype, work):
         "solve_s": round(el, 4), "dtype": a.dtype,
         "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
                    "chains": a.chains, "inner_order": res.info.get("inner_order", a.inner_order),
-                   "link_gbps_model": a.sim_link_gbps},
+                   "link_gbps_model": a.sim_link_gbps, "exchange": comm.exchange},
         "comm": res.info.get("comm"),
         "qr_seconds": res.info.get("qr_seconds"),
         "sim_bytes_per_exchange": comm.bytes_moved // max(comm.exchanges, 1),
@@ -498,6 +499,9 @@ def main():
                         "comm_ms / exposed_comm_ms (adds events; off for headline runs)")
     p.add_argument("--inject-fault", default=None, metavar="RANK:SWEEP",
                    help="failure-detection test: that rank exits abruptly after that sweep")
+    p.add_argument("--exchange", default="auto", choices=["auto", "direct", "spread"],
+                   help="half super-block transfer: one link (direct) or all links, relayed "
+                        "(spread); auto = spread from 4 GPUs")
     p.add_argument("--simulate-P", type=int, default=0)
     p.add_argument("--simulate-rank", type=int, default=0)
     p.add_argument("--sim-sweeps", type=int, default=3)
@@ -524,7 +528,7 @@ def main():
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
                             stagger=bool(a.stagger), precondition=a.precondition,
                             inner_order=a.inner_order,
-                            progress=a.progress, comm_timing=a.comm_timing)
+                            progress=a.progress, comm_timing=a.comm_timing, exchange=a.exchange)
     if a.inject_fault:
         r_, s_ = (int(x) for x in a.inject_fault.split(":"))
         cfg.extra["fault_exit"] = (r_, s_)
@@ -636,6 +640,7 @@ def main():
                 "inner_order": last.info.get("inner_order", a.inner_order),
                 "staggered": bool(a.stagger),
                 "root_owned": a.root_owned,
+                "exchange": last.info.get("exchange", a.exchange),
             },
             "sweeps": sweeps,
             "converged": conv,

@@ -71,6 +71,11 @@ class SolverConfig:
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     progress: bool = False          # rank 0 prints one line per sweep to stderr
     comm_timing: bool = False       # distributed: HIP-event timing of every exchange
+    # distributed, pipelined: how a half super-block travels between GPUs.
+    # direct: one grouped send/recv (one xGMI link); spread: cut into P-1
+    # chunks, relayed over all links in two phases (parallel/spread.py);
+    # auto: spread from 4 GPUs up
+    exchange: str = "auto"
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
@@ -81,6 +86,8 @@ class SolverConfig:
                              f"got {self.chains}")
         if self.max_inner_sweeps < 0 or self.max_sweeps < 0:
             raise ValueError("max_sweeps / max_inner_sweeps must be >= 0")
+        if self.exchange not in ("auto", "direct", "spread"):
+            raise ValueError(f"exchange must be auto, direct or spread, got {self.exchange!r}")
 
     def bf16_mode(self, A: torch.Tensor | None = None) -> bool:
         """bf16 problem: bf16 in/out, fp32 master copies of A and V, block

@@ -254,13 +254,16 @@ class SimCommunicator:
 
     ``link_gbps`` > 0 pads every exchange on the comm stream with a device
     spin of the modelled transfer time (bytes of the larger direction over
-    the link bandwidth), so the overlap with compute can be studied.
+    the link bandwidth), so the overlap with compute can be studied.  With
+    ``exchange="spread"`` the modelled time is that of the two relayed phases
+    over all links (parallel/spread.py, 2/(P-1) of the direct time); the
+    device copies stay direct.
     """
 
     backend = "sim"
 
     def __init__(self, world: int, rank: int, device: torch.device, seed_fn=None,
-                 link_gbps: float = 0.0):
+                 link_gbps: float = 0.0, exchange: str = "direct"):
         if not (0 <= rank < world):
             raise ValueError(f"rank {rank} not in world {world}")
         self.world, self.rank = int(world), int(rank)
@@ -269,6 +272,9 @@ class SimCommunicator:
         self.owns_group = False
         self.seed_fn = seed_fn
         self.link_gbps = float(link_gbps)
+        from .spread import modelled_time_factor, resolve_exchange
+        self.exchange = resolve_exchange(exchange, self.world)
+        self.link_factor = modelled_time_factor(self.world) if self.exchange == "spread" else 1.0
         self._ring: dict = {}
         self.bytes_moved = 0
         self.exchanges = 0
@@ -293,7 +299,7 @@ class SimCommunicator:
         self.exchanges += 1
         if self.link_gbps > 0 and self.device.type == "cuda":
             from ..ops import kernels as K
-            K.spin_ns(self.device, nbytes / (self.link_gbps * 1e9) * 1e9)
+            K.spin_ns(self.device, nbytes * self.link_factor / (self.link_gbps * 1e9) * 1e9)
 
     def sendrecv(self, sends: list, recvs: list):
         self._swap(sends, recvs)

@@ -292,7 +292,7 @@ class DistributedBlockJacobi(Solver):
         bufs = (rA, rV, rD)
         if pipelined:
             ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
-                                  parts=splan.parts)
+                                  parts=splan.parts, exchange=cfg.exchange)
 
             def run_steps(pairs, modes, slot):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
@@ -353,6 +353,7 @@ class DistributedBlockJacobi(Solver):
         t_total = time.perf_counter() - t0
         info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "inner_order": inner,
+                "exchange": ex.exchange if pipelined else "direct",
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
         if pipelined and P > 1:
             info["comm"] = ex.comm_summary()

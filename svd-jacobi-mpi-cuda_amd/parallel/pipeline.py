@@ -36,6 +36,7 @@ import numpy as np
 import torch
 
 from .schedule import round_robin
+from .spread import relay_chunk, resolve_exchange, spread_ops
 
 
 @dataclass
@@ -305,6 +306,10 @@ class PipelineExecutor:
     :meth:`canonicalize` before reading the result: it moves the halves back
     to buffer 2 slot + half, i.e. rows [s B, (s+1) B) = slot s.
 
+    ``exchange="spread"`` (parallel/spread.py) moves every half over all
+    xGMI links in two relayed phases instead of the one direct link; the
+    data that arrives is identical, bit for bit.
+
     Exchange timing (``timing=True``, device runs with a stream-ordered
     communicator): every half exchange is bracketed on the comm stream by two
     timing events (issue after its producers' events, arrival of both
@@ -316,7 +321,7 @@ class PipelineExecutor:
     (:func:`exposed_time`) -- the part of the exchanges on the critical path."""
 
     def __init__(self, comm, streams, At, Vt, D, k: int, W: int, tour, timing: bool = False,
-                 parts: int = 2):
+                 parts: int = 2, exchange: str = "direct"):
         if parts != 2:
             raise ValueError("the pipelined executor moves super-blocks in halves")
         self.comm, self.streams = comm, streams
@@ -340,6 +345,12 @@ class PipelineExecutor:
         self._waits = []     # (consumer-ready event, arrival event) per consume
         self._busy = []      # (start event, end event) per task
         self.bytes_sent = 0
+        self.bytes_relayed = 0
+        # the simulated communicator models a spread exchange by its time only
+        self.exchange = resolve_exchange(exchange, comm.world)
+        self.spread = self.exchange == "spread" and getattr(comm, "backend", "") != "sim"
+        self._relay = {}     # message index -> (P, chunk) relay buffer
+        self._spread_ops = {}
 
     @staticmethod
     def storage_columns(B: int, distributed: bool) -> int:
@@ -456,8 +467,12 @@ class PipelineExecutor:
             raise RuntimeError("exchange on a single rank")
         # from here on (host program order) the half lives in the received buffer
         self.layout.loc[x][hh], self.layout.spare[hh] = in_b, out_b
+        phases = [(sends, recvs)]
+        if self.spread:
+            phases = self._spread_phases(r, [t for t, _ in sends], [t for t, _ in recvs])
         if not self.cuda:
-            comm.sendrecv(sends, recvs)
+            for ps, pr in phases:
+                comm.sendrecv(ps, pr)
             last.pop((x, hh), None)
             return
         cs = self.comm_stream
@@ -469,7 +484,17 @@ class PipelineExecutor:
             # data ready on the host side first.  RCCL needs none of this.
             cs.synchronize()
             with torch.cuda.stream(cs):
-                pending[(x, hh)] = comm.isendrecv(sends, recvs)
+                if len(phases) > 1:
+                    # relayed: both phases complete here -- the relay buffers
+                    # are reused by the next exchange, which this host-driven
+                    # path would otherwise start while forwards still read them
+                    for ps, pr in phases:
+                        for w in comm.isendrecv(ps, pr):
+                            w.wait()
+                        torch.cuda.synchronize(self.At.device)
+                    pending[(x, hh)] = []
+                else:
+                    pending[(x, hh)] = comm.isendrecv(sends, recvs)
             return
         # Stream-ordered (RCCL): the comm stream issues the grouped send/recv
         # after the producers' events, then waits (device-side) for both
@@ -481,13 +506,51 @@ class PipelineExecutor:
             if self.timing:
                 t_issue = torch.cuda.Event(enable_timing=True)
                 t_issue.record(cs)
-            for w in comm.isendrecv(sends, recvs):
-                w.wait()
+            for ps, pr in phases:  # phase 2 is stream-ordered after phase 1
+                for w in comm.isendrecv(ps, pr):
+                    w.wait()
             arrived = self._event()
             arrived.record(cs)
         if self.timing:
             self._spans.append((t_issue, arrived))
         pending[(x, hh)] = arrived
+
+    def _spread_phases(self, r: int, outs: list, ins: list) -> list:
+        """[(sends, recvs)] of the two relayed phases of round r's exchange
+        (parallel/spread.py) on flat views of the outgoing / incoming half
+        buffers; the norms (tiny) go directly."""
+        comm = self.comm
+        P = comm.world
+        flat_out = [t.reshape(-1) for t in outs]
+        flat_in = [t.reshape(-1) for t in ins]
+        sizes = [t.numel() for t in flat_out]
+        flags = [t.dim() == 2 for t in outs]  # At / Vt spread, D direct
+        key = (r, tuple(sizes))
+        ops = self._spread_ops.get(key)
+        if ops is None:
+            ops = spread_ops(comm.rank, self.tour.send_to[r], sizes, flags)
+            self._spread_ops[key] = ops
+
+        def relay(mi):
+            buf = self._relay.get(mi)
+            if buf is None:
+                buf = torch.empty(P, relay_chunk(sizes[mi], P), dtype=flat_out[mi].dtype,
+                                  device=flat_out[mi].device)
+                self._relay[mi] = buf
+            return buf
+
+        def tensor(op):
+            mi, (a, b), peer, where = op
+            if where == "out":
+                return flat_out[mi][a:b], peer
+            if where == "in":
+                return flat_in[mi][a:b], peer
+            return relay(mi)[where[1], :b - a], peer
+
+        p1 = ([tensor(o) for o in ops.p1_send], [tensor(o) for o in ops.p1_recv])
+        p2 = ([tensor(o) for o in ops.p2_send], [tensor(o) for o in ops.p2_recv])
+        self.bytes_relayed += sum(t.numel() * t.element_size() for t, _ in p2[0])
+        return [p1, p2]
 
     def _consume(self, hv, pending):
         got = pending.pop(hv, None)
@@ -516,7 +579,8 @@ class PipelineExecutor:
 
     def comm_summary(self) -> dict:
         """Exchange timing of every sweep run so far (synchronises)."""
-        out = {"exchanges": len(self._spans), "bytes_sent": int(self.bytes_sent)}
+        out = {"exchanges": len(self._spans), "bytes_sent": int(self.bytes_sent),
+               "exchange": self.exchange, "bytes_relayed": int(self.bytes_relayed)}
         if not self.timing or self._t0 is None:
             return out
         torch.cuda.synchronize(self.At.device)

@@ -44,6 +44,24 @@ def main():
                 json.dump({"ok_ranks": float(t[0]), "world": comm.world}, f)
         comm.destroy()
         return
+    if mode == "exchcmp":  # spread (relayed over all links) vs direct exchange: same bits
+        got = {}
+        for ex in ("direct", "spread"):
+            cfg.exchange = ex
+            res = DistributedBlockJacobi(cfg, comm).solve(A if comm.rank == 0 else None)
+            got[ex] = res
+        if comm.rank == 0:
+            d, s_ = got["direct"], got["spread"]
+            with open(out, "w") as f:
+                json.dump({"u_diff": float((d.U - s_.U).abs().max()),
+                           "s_diff": float((d.S - s_.S).abs().max()),
+                           "v_diff": float((d.V - s_.V).abs().max()),
+                           "sweeps": [d.sweeps, s_.sweeps],
+                           "exchange": [d.info["exchange"], s_.info["exchange"]],
+                           "relayed": s_.info["comm"]["bytes_relayed"],
+                           "world": comm.world}, f)
+        comm.destroy()
+        return
     if mode == "otf":  # on-the-fly generated input through the public API
         res = svdj.svd_on_the_fly(m, n, lambda c0, c1: A[:, c0:c1], comm=comm,
                                   dtype=torch.float64, config=cfg)

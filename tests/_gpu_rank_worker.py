@@ -25,7 +25,8 @@ def main():
     comm = Communicator(timeout_s=120)
     dev = comm.device
     cfg = svdj.SolverConfig(block=W, dtype=torch.float32, chains=chains, comm_timing=True,
-                            precondition="none")
+                            precondition="none",
+                            exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"))
     solver = DistributedBlockJacobi(cfg, comm)
     g = torch.Generator(device=dev).manual_seed(5)
     m = 4 * n if mode == "qr" else n
@@ -41,6 +42,7 @@ def main():
         torch.save({"U": res.U.cpu(), "S": res.S.cpu(), "V": res.V.cpu(), "A": A.cpu(),
                     "sweeps": res.sweeps, "converged": res.converged, "history": res.history,
                     "backend": comm.backend, "world": comm.world,
+                    "exchange": res.info.get("exchange"),
                     "comm": json.dumps(res.info.get("comm"))}, out)
     comm.destroy()
 

@@ -64,6 +64,67 @@ def test_isend_irecv_ring(world, tmp_path):
     assert rep["ok_ranks"] == world
 
 
+@pytest.mark.parametrize("world,m,n", [(4, 300, 256), (5, 340, 320)])
+def test_spread_exchange_matches_direct(world, m, n, tmp_path):
+    """parallel/spread.py: every half relayed over all links in two phases
+    delivers exactly the direct exchange's data, so the solves are bitwise
+    equal (and the relays really carried bytes)."""
+    rep = _run(world, m, n, 32, tmp_path, mode="exchcmp")
+    assert rep["exchange"] == ["direct", "spread"] and rep["relayed"] > 0, rep
+    assert rep["u_diff"] == 0.0 and rep["s_diff"] == 0.0 and rep["v_diff"] == 0.0, rep
+    assert rep["sweeps"][0] == rep["sweeps"][1]
+
+
+def test_spread_ops_deliver_every_chunk_once():
+    """Simulate the two phases of spread_ops for every rank of every
+    tournament round at P = 3..8: each directed pair's sends and receives
+    match one to one in order and size, relays forward what they received,
+    and every rank ends with exactly the message its sender sent."""
+    import numpy as np
+
+    from svdj.parallel.schedule import tournament
+    from svdj.parallel.spread import spread_ops
+
+    for P in range(3, 9):
+        tour = tournament(P)
+        sizes, flags = [37, 5, 23], [True, False, True]
+        for r in range(1, tour.rounds):
+            send_to = [int(x) for x in tour.send_to[r]]
+            ops = [spread_ops(g, send_to, sizes, flags) for g in range(P)]
+            out = {g: [np.arange(n) + 1000 * g + 100 * mi for mi, n in enumerate(sizes)]
+                   for g in range(P)}
+            inc = {g: [np.full(n, -1) for n in sizes] for g in range(P)}
+            relay = {g: {} for g in range(P)}
+
+            def run(phase):
+                sends = {}
+                for g in range(P):
+                    for mi, (a, b), peer, where in getattr(ops[g], f"p{phase}_send"):
+                        data = out[g][mi][a:b] if where == "out" else relay[g][(mi, where[1])]
+                        sends.setdefault((g, peer), []).append((mi, data.copy()))
+                for g in range(P):
+                    recvd = {}
+                    for mi, (a, b), peer, where in getattr(ops[g], f"p{phase}_recv"):
+                        q = sends[(peer, g)]
+                        i = recvd.get(peer, 0)
+                        recvd[peer] = i + 1
+                        smi, data = q[i]
+                        assert smi == mi and len(data) == b - a
+                        if where == "in":
+                            inc[g][mi][a:b] = data
+                        else:
+                            relay[g][(mi, where[1])] = data
+                    for peer, cnt in recvd.items():
+                        assert cnt == len(sends[(peer, g)])
+
+            run(1)
+            run(2)
+            for g in range(P):
+                src = send_to.index(g)
+                for mi in range(3):
+                    assert (inc[g][mi] == out[src][mi]).all(), (P, r, g, mi)
+
+
 def test_svd_on_the_fly_api(tmp_path):
     rep = _run(2, 170, 128, 32, tmp_path, mode="otf")
     assert rep["converged"] and rep["residual_rel"] < 1e-12, rep

@@ -33,8 +33,9 @@ def _port():
     return p
 
 
-def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=150):
-    env = dict(os.environ, SVDJ_SHARED_GPU="1", SVDJ_COMM_BACKEND=backend, OMP_NUM_THREADS="2")
+def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=150, exchange="auto"):
+    env = dict(os.environ, SVDJ_SHARED_GPU="1", SVDJ_COMM_BACKEND=backend, OMP_NUM_THREADS="2",
+               SVDJ_TEST_EXCHANGE=exchange)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(n), str(W),
            str(chains), mode, str(out)]
@@ -66,6 +67,19 @@ def test_rccl_matches_gloo_bitwise(P, tmp_path):
         assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
     _check_accuracy(r)
     assert '"comm_ms"' in r["comm"] and '"exposed_comm_ms"' in r["comm"], r["comm"]
+
+
+def test_rccl_spread_exchange_matches_direct(tmp_path):
+    """4 RCCL ranks: every half relayed over all peers in two grouped phases
+    (parallel/spread.py, the default from 4 GPUs) gives bitwise the result
+    of the direct one-link exchange."""
+    s = _run(4, "nccl", tmp_path / "spread.pt", exchange="spread")
+    d = _run(4, "nccl", tmp_path / "direct.pt", exchange="direct")
+    assert s["exchange"] == "spread" and d["exchange"] == "direct"
+    assert '"bytes_relayed"' in s["comm"] and s["sweeps"] == d["sweeps"]
+    for k in ("U", "S", "V"):
+        assert torch.equal(s[k], d[k]), (k, float((s[k] - d[k]).abs().max()))
+    _check_accuracy(s)
 
 
 def test_rccl_root_owned_scatter_gather(tmp_path):
