@@ -357,6 +357,7 @@ def run_native(a, dtype, work):
     p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
     p.hist = C.cast(hist, C.POINTER(C.c_double))
     p.stagger = 1 if a.stagger else 0
+    p.exchange = {"auto": 0, "direct": 1, "spread": 2}[a.exchange]
     p.timeout_s = float(timeout)
     p.comm_timing = 1 if a.comm_timing else 0
     p.fault_rank, p.fault_sweep = -1, -1
@@ -430,6 +431,7 @@ def run_native(a, dtype, work):
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
                        "mma": "native", "precondition": "none", "chains": 2,
                        "inner_order": a.inner_order,
+                       "exchange": a.exchange,
                        "staggered": bool(a.stagger), "root_owned": False},
             "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],

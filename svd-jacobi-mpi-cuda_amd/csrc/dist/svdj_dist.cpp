@@ -427,6 +427,9 @@ struct Watchdog {
 
 struct svdj_dist_handle_t {
   int rank, world, dtype, W, m_pad, n_v, B, k, hk, hB, has_v, timing;
+  bool spread = false;           // exchanges relayed over all links (parallel/spread.py)
+  void* relay[2] = {nullptr, nullptr};  // A / V relay chunks, one row per source rank
+  size_t relay_n[2] = {0, 0};           // elements per row
   ncclComm_t comm;
   hipStream_t st[2], sc;
   bool own_sc = false;
@@ -518,6 +521,8 @@ void handle_free(svdj_dist_handle_t* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->own_sc && h->sc) (void)hipStreamDestroy(h->sc);
   (void)hipFree(h->pairs_pool);
+  (void)hipFree(h->relay[0]);
+  (void)hipFree(h->relay[1]);
   (void)hipFree(h->ws[0]);
   (void)hipFree(h->ws[1]);
   (void)hipFree(h->metric);
@@ -553,6 +558,16 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
     if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);
   if (!rc && hipMalloc((void**)&h->metric, 4 * sizeof(uint32_t)) != hipSuccess)
     rc = fail(-100, "hipMalloc(metric) failed");
+  if (p->exchange < 0 || p->exchange > 2) rc = rc ? rc : fail(-2, "exchange %d (0 auto, 1 direct, 2 spread)", p->exchange);
+  h->spread = h->world > 2 && (p->exchange == 2 || (p->exchange == 0 && h->world >= 4));
+  if (h->spread) {  // chunk rows: ceil(message / (P - 1)) elements
+    const size_t msg[2] = {(size_t)h->hB * h->m_pad, h->has_v ? (size_t)h->hB * h->n_v : 0};
+    for (int i = 0; i < 2 && !rc; ++i) {
+      h->relay_n[i] = (msg[i] + h->world - 2) / (h->world - 1);
+      if (msg[i] && hipMalloc(&h->relay[i], h->relay_n[i] * h->world * h->es) != hipSuccess)
+        rc = fail(-100, "hipMalloc(relay %zu) failed", h->relay_n[i] * h->world * h->es);
+    }
+  }
   if (!rc && !h->sc && h->world > 1) {
     if (hipStreamCreateWithFlags(&h->sc, hipStreamNonBlocking) != hipSuccess)
       rc = fail(-100, "comm stream creation failed");
@@ -712,16 +727,82 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         if (h->timing) HIPC(hipEventRecord(h->ev_start[gr.a], sc));
         std::unique_lock<std::mutex> lk(wd.mu);
         if (wd.fired.load()) return fail(-300, "%s", wd.why);
-        NCCLC(ncclGroupStart());
-        NCCLC(ncclSend(buf_ptr(p->At, h->m_pad, out_b), (size_t)hB * h->m_pad, nt, dst, comm, sc));
-        NCCLC(ncclSend((char*)p->D + (size_t)out_b * hB * es, (size_t)hB, nt, dst, comm, sc));
-        NCCLC(ncclRecv(buf_ptr(p->At, h->m_pad, in_b), (size_t)hB * h->m_pad, nt, src, comm, sc));
-        NCCLC(ncclRecv((char*)p->D + (size_t)in_b * hB * es, (size_t)hB, nt, src, comm, sc));
-        if (p->Vt) {
-          NCCLC(ncclSend(buf_ptr(p->Vt, h->n_v, out_b), (size_t)hB * h->n_v, nt, dst, comm, sc));
-          NCCLC(ncclRecv(buf_ptr(p->Vt, h->n_v, in_b), (size_t)hB * h->n_v, nt, src, comm, sc));
+        // messages in the order of pipeline.py: A half, norms, V half
+        struct Msg {
+          char *out, *in;
+          size_t n;
+          char* relay;  // non-null: spread
+          size_t relay_n;
+        } msgs[3];
+        int nm = 0;
+        msgs[nm++] = {buf_ptr(p->At, h->m_pad, out_b), buf_ptr(p->At, h->m_pad, in_b),
+                      (size_t)hB * h->m_pad, h->spread ? (char*)h->relay[0] : nullptr, h->relay_n[0]};
+        msgs[nm++] = {(char*)p->D + (size_t)out_b * hB * es, (char*)p->D + (size_t)in_b * hB * es,
+                      (size_t)hB, nullptr, 0};
+        if (p->Vt)
+          msgs[nm++] = {buf_ptr(p->Vt, h->n_v, out_b), buf_ptr(p->Vt, h->n_v, in_b),
+                        (size_t)hB * h->n_v, h->spread ? (char*)h->relay[1] : nullptr,
+                        h->relay_n[1]};
+        // spread (parallel/spread.py): chunk j of P-1 near-equal pieces; chunk 0
+        // direct, chunk j >= 1 via the j-th rank not in {sender, receiver}
+        auto piece = [&](size_t n, int j, size_t& a, size_t& len) {
+          const size_t base = n / (P - 1), rem = n % (P - 1);
+          a = j * base + ((size_t)j < rem ? (size_t)j : rem);
+          len = base + ((size_t)j < rem ? 1 : 0);
+        };
+        auto relay_index = [&](int s, int d, int q) {
+          int j = 0;
+          for (int x = 0; x < P; ++x) {
+            if (x == s || x == d) continue;
+            ++j;
+            if (x == q) return j;
+          }
+          return -1;
+        };
+        size_t a0, ln;
+        NCCLC(ncclGroupStart());  // direct messages / phase 1
+        for (int i = 0; i < nm; ++i) {
+          const Msg& M = msgs[i];
+          if (!M.relay) {
+            NCCLC(ncclSend(M.out, M.n, nt, dst, comm, sc));
+            NCCLC(ncclRecv(M.in, M.n, nt, src, comm, sc));
+            continue;
+          }
+          piece(M.n, 0, a0, ln);
+          NCCLC(ncclSend(M.out + a0 * es, ln, nt, dst, comm, sc));
+          for (int q = 0, j = 0; q < P; ++q) {
+            if (q == g || q == dst) continue;
+            piece(M.n, ++j, a0, ln);
+            NCCLC(ncclSend(M.out + a0 * es, ln, nt, q, comm, sc));
+          }
+          piece(M.n, 0, a0, ln);
+          NCCLC(ncclRecv(M.in + a0 * es, ln, nt, src, comm, sc));
+          for (int s = 0; s < P; ++s) {  // sources this rank relays for
+            if (s == g || s == src) continue;
+            piece(M.n, relay_index(s, tour.to(a.round, s), g), a0, ln);
+            NCCLC(ncclRecv(M.relay + (size_t)s * M.relay_n * es, ln, nt, s, comm, sc));
+          }
         }
         NCCLC(ncclGroupEnd());
+        if (h->spread) {  // phase 2: forward the relayed chunks, receive ours
+          NCCLC(ncclGroupStart());
+          for (int i = 0; i < nm; ++i) {
+            const Msg& M = msgs[i];
+            if (!M.relay) continue;
+            for (int s = 0; s < P; ++s) {
+              if (s == g || s == src) continue;
+              const int d = tour.to(a.round, s);
+              piece(M.n, relay_index(s, d, g), a0, ln);
+              NCCLC(ncclSend(M.relay + (size_t)s * M.relay_n * es, ln, nt, d, comm, sc));
+            }
+            for (int q = 0, j = 0; q < P; ++q) {
+              if (q == src || q == g) continue;
+              piece(M.n, ++j, a0, ln);
+              NCCLC(ncclRecv(M.in + a0 * es, ln, nt, q, comm, sc));
+            }
+          }
+          NCCLC(ncclGroupEnd());
+        }
         lk.unlock();
         // received in place: from here on (issue order) the half lives in in_b;
         // in_b's last readers were waited for by the exchange that freed it

@@ -6,7 +6,7 @@
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
 //                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
-//                  [--no-v]
+//                  [--exchange auto|direct|spread] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH] [--comm-timing] [--inject-fault RANK:SWEEP] [--keep-going]
 //
@@ -55,6 +55,7 @@ namespace {
 
 struct Opts {
   int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 3;  // auto
+  int exchange = 0;  // auto
   int fault_rank = -1, fault_sweep = -1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
@@ -163,6 +164,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.max_sweeps = o.max_sweeps;
   p.mma = o.mma;
   p.inner_order = o.inner;
+  p.exchange = o.exchange;
   p.stream_a = sa;
   p.stream_b = sb;
   p.stream_comm = sc;
@@ -367,7 +369,10 @@ int main(int argc, char** argv) {
     else if (a == "--verify") o.verify = true;
     else if (a == "--timeout") o.timeout = std::atof(next());
     else if (a == "--warmup") o.warmup = std::atoi(next());
-    else if (a == "--inner") {
+    else if (a == "--exchange") {
+      const std::string v = next();
+      o.exchange = v == "spread" ? 2 : (v == "direct" ? 1 : 0);
+    } else if (a == "--inner") {
       const std::string v = next();
       o.inner = v == "auto" ? 3 : (v == "cross" ? 2 : (v == "bipartite" ? 1 : 0));
     }

@@ -10,8 +10,8 @@
 // stop test.  The exchange is pipelined as in parallel/pipeline.py: each
 // super-block moves in two halves with grouped ncclSend/ncclRecv on a comm
 // stream as soon as the tasks touching that half are done, received in place
-// into a spare half buffer, and consumers wait on the arrival event -- the
-// host never blocks inside a sweep.  A watchdog thread aborts the
+// into a spare half buffer (from 4 GPUs relayed over all xGMI links), and
+// consumers wait on the arrival event -- the host never blocks inside a sweep.  A watchdog thread aborts the
 // communicator on an RCCL async error or when no sweep finishes in time.
 #pragma once
 #include <stddef.h>
@@ -67,6 +67,10 @@ typedef struct {
                               // (svdj_choose_inner_order of the half super-block pairs)
   int stagger;                // 1: the two chains of a group offset by an EVD
                               // (svdj_block_steps2); 0 (default): issued independently
+  int exchange;               // half super-block transfer: 0 auto (spread from 4 ranks),
+                              // 1 direct (one grouped send/recv, one xGMI link), 2 spread
+                              // (P-1 chunks relayed over all links in two grouped phases,
+                              // parallel/spread.py)
   void* stream_a;             // two compute streams (distinct)
   void* stream_b;
   void* stream_comm;          // exchange stream, or NULL (created by the handle).  HIP maps

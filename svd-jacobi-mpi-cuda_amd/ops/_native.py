@@ -140,7 +140,8 @@ class DistProblem(C.Structure):
                 ("W", c_int), ("m_pad", c_int), ("n_v", c_int), ("B", c_int),
                 ("At", c_void_p), ("Vt", c_void_p), ("D", c_void_p), ("held", C.c_int32 * 2),
                 ("tol", c_double), ("tol_mode", c_int), ("max_sweeps", c_int), ("mma", c_int),
-                ("inner_order", c_int), ("stagger", c_int), ("stream_a", c_void_p),
+                ("inner_order", c_int), ("stagger", c_int), ("exchange", c_int),
+                ("stream_a", c_void_p),
                 ("stream_b", c_void_p), ("stream_comm", c_void_p), ("timeout_s", c_double),
                 ("comm_timing", c_int), ("fault_rank", c_int), ("fault_sweep", c_int),
                 ("handle", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),

@@ -106,3 +106,21 @@ def test_native_dist_reference_triangular_input_converges():
     assert "converged: 1" in out, out
     assert _value(out, "||A-USVt||_F/||A||_F:") < 1e-12, out
     assert _value(out, "||V^TV-I||_F:") < 1e-9, out
+
+
+def test_native_spread_exchange_matches_direct():
+    """Native engine, 4 RCCL ranks: the spread exchange (every half relayed
+    over all peers in two grouped phases, svdj_dist_problem.exchange = 2)
+    delivers the direct exchange's bits -- same sweeps, same off value, same
+    residual to the printed digits."""
+    outs = {}
+    for ex in ("direct", "spread"):
+        r = subprocess.run([_exe(), "1024", "--np", "4", "--shared-gpu", "--dtype", "f32",
+                            "--input", "dense", "--verify", "--exchange", ex, "--timeout", "120"],
+                           capture_output=True, text=True, timeout=170)
+        out = r.stdout + r.stderr
+        assert r.returncode == 0 and "converged: 1" in out, out[-4000:]
+        outs[ex] = out
+    for key in ("sweeps:", "||A-USVt||_F:", "||U^TU-I||_F:", "||V^TV-I||_F:"):
+        assert outs["direct"].split(key)[1].split("\n")[0] == \
+            outs["spread"].split(key)[1].split("\n")[0], key
