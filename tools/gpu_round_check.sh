@@ -1,13 +1,15 @@
 # GPU check used during development: gpu tests, default bench, kernel profile.
 # Usage (from the repo root, via gpurun):  bash tools/gpu_round_check.sh [N]
 set -o pipefail
-# Same environment as the driver: no SVDJ_* overrides (autobuild on; in-tree libs are current).
+# Same environment as the driver: no SVDJ_* overrides (autobuild on; in-tree libs are
+# current) and pytest.ini's per-test timeout.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=${1:-16384}
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout-method thread --durations=20 \
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
+tail -25 gpurun_out/pytest_gpu.log
+[ -n "$NO_BENCH" ] && exit 0
 timeout -k 10 300 python bench.py --n $N --steps 1 --warmup 1 > gpurun_out/bench_$N.log 2>&1 \
   || { tail -20 gpurun_out/bench_$N.log; exit 1; }
 tail -1 gpurun_out/bench_$N.log
