@@ -25,7 +25,7 @@ def main():
     comm = Communicator(timeout_s=120)
     dev = comm.device
     cfg = svdj.SolverConfig(block=W, dtype=torch.float32, chains=chains, comm_timing=True,
-                            precondition="none",
+                            precondition="none", progress=True,
                             exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"))
     solver = DistributedBlockJacobi(cfg, comm)
     g = torch.Generator(device=dev).manual_seed(5)

@@ -33,13 +33,17 @@ def _port():
     return p
 
 
-def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=150, exchange="auto"):
+def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=300, exchange="auto"):
     env = dict(os.environ, SVDJ_SHARED_GPU="1", SVDJ_COMM_BACKEND=backend, OMP_NUM_THREADS="2",
                SVDJ_TEST_EXCHANGE=exchange)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(n), str(W),
            str(chains), mode, str(out)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:  # report what the ranks printed (sweep progress)
+        out_ = (e.stdout or b"")[-3000:], (e.stderr or b"")[-3000:]
+        pytest.fail(f"{backend} P={P} timed out after {timeout} s:\n{out_[0]!r}\n{out_[1]!r}")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return torch.load(out, weights_only=False)
 
