@@ -153,8 +153,8 @@ extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* n
 extern "C" int svdj_dist_choose_block(int dtype, int world, int m, int n) {
   // models/block.py choose_block (measurements there)
   const int per_gpu = n / (world > 0 ? world : 1);
-  if (dtype == 1) return (m >= 12288 && per_gpu >= 4096) ? 64 : 32;
-  return (m >= 8192 && per_gpu >= 2048) ? 64 : 32;
+  if (dtype == 1) return (m >= 6144 && per_gpu >= 2048) ? 64 : 32;
+  return per_gpu >= 1024 ? 64 : 32;
 }
 
 extern "C" int svdj_dist_initial_held(int world, int rank, int32_t held[2]) {

@@ -182,7 +182,7 @@ int main(int argc, char** argv) {
     svdj_ref_triu_input(m, n, A.data(), m, seed);
   const int mma_code = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
   if (W == 0)  // models/block.py choose_block
-    W = dtype == "f32" ? ((m >= 8192 && n >= 2048) ? 64 : 32) : ((m >= 12288 && n >= 4096) ? 64 : 32);
+    W = dtype == "f32" ? (n >= 1024 ? 64 : 32) : ((m >= 6144 && n >= 2048) ? 64 : 32);
   if (dtype == "f32")
     return run<float>(m, n, A, method, W, max_sweeps, tol, mma_code, inner_order, verify, report_dir);
   return run<double>(m, n, A, method, W, max_sweeps, tol, 0, inner_order, verify, report_dir);

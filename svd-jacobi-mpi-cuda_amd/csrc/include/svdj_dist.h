@@ -33,9 +33,9 @@ int svdj_dist_comm_destroy(void* comm);
 // super-blocks of B columns (B/W even); row counts padded to 128.
 int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* ncols, int* m_pad, int* n_v);
 
-// Default block width (models/block.py choose_block): fp32 64 when m >= 8192
-// and a GPU holds >= 2048 columns, fp64 64 when m >= 12288 and >= 4096
-// columns per GPU, else 32.
+// Default block width (models/block.py choose_block): fp32 64 when a GPU
+// holds >= 1024 columns, fp64 64 when m >= 6144 and >= 2048 columns per GPU,
+// else 32.
 int svdj_dist_choose_block(int dtype, int world, int m, int n);
 
 // Super-block ids held by `rank` at the start of a sweep (round 0 placement).

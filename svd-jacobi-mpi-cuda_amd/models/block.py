@@ -20,21 +20,26 @@ def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     """Block width W for ``n`` columns per GPU of ``m`` rows.
 
     W=64 halves the steps and the per-byte traffic of the Gram and the apply,
-    but its EVD is slower and a step holds half as many pairs.  It pays when
-    the rows are long (the Gram and apply dominate) and a half task still
-    has enough pairs.  Measured on MI355X with the bipartite cross-step EVD
-    (profiles/r2_simgrid2), time per solve or per sweep, W=32 / W=64:
-      * fp32, 1 GPU n x n: 4096 0.179 / 0.186 s, 8192 1.13 / 0.88 s,
-        12288 3.92 / 2.63 s;
-      * fp32 rank plans, ms per sweep: 16384^2 on P=2 345 / 216, P=4
-        159 / 125, P=8 (2048 columns per GPU) 83 / 69; 8192^2 on P=8 (1024
-        columns) 22.2 / 26.2; 65536^2 on P=8 4268 / 1787;
-      * fp64, 1 GPU: 5000 0.54 / 0.80 s, 8192 2.47 / 2.56 s, 16384 17.8 /
-        16.5 s (the fp64 W=64 EVD keeps a 2x larger G in LDS).
+    but its EVD is slower and a step holds half as many pairs.  Since the
+    low-latency cross EVD (choose_inner_order "cross" for <= 16 W=64 pairs
+    per step, round 3) the W=64 EVD no longer dominates small problems, and
+    W=64 wins almost everywhere.  Measured on MI355X, round 3
+    (profiles/r3_blockw), W=32 / W=64:
+      * fp32, 1 GPU n x n, ms per solve: 512 15.7 / 12.1, 1024 21.5 / 21.1,
+        2048 50.3 / 41.6, 3072 102 / 92, 4096 162 / 149, 6144 454 / 390;
+      * fp32 rank plans, ms per sweep: 8192^2 P=8 (1024 columns per GPU)
+        20.0 / 15.2, P=4 23.0 / 22.3; 4096^2 P=2 10.9 / 8.6, P=8 (512
+        columns) 10.0 / 12.4; 2048^2 P=4 (512) 4.9 / 4.4;
+      * fp64, 1 GPU, ms per solve: 5000 516 / 559, 6144 926 / 884, 8192
+        2420 / 2063, 10000 3917 / 3583; rank plans, ms per sweep: 5000^2
+        P=2 (2500 columns) 22.9 / 25.1, 10000^2 P=2 147 / 126, 16384^2 P=8
+        (2048 columns) 164 / 141.
+    Rule: fp32 W=64 from 1024 columns per GPU; fp64 W=64 from m >= 6144 rows
+    and 2048 columns per GPU (the fp64 W=64 EVD keeps a 2x larger G in LDS).
     """
     if dtype == torch.float64:
-        return 64 if (m >= 12288 and n >= 4096) else 32
-    return 64 if (m >= 8192 and n >= 2048) else 32
+        return 64 if (m >= 6144 and n >= 2048) else 32
+    return 64 if n >= 1024 else 32
 
 
 def choose_inner_order(W: int, pairs_per_step: int) -> str:

@@ -126,8 +126,9 @@ def test_native_block_rule_matches_python():
     choose = svdj.models.block.choose_block
     for dt, code in ((torch.float32, 0), (torch.float64, 1)):
         for world in (1, 2, 4, 8):
-            for m, n in ((4096, 4096), (8192, 8192), (12288, 12288), (16384, 16384),
-                         (32768, 8192), (65536, 65536), (20000, 20000)):
+            for m, n in ((512, 512), (2048, 2048), (4096, 4096), (5000, 5000), (6144, 6144),
+                         (8192, 8192), (12288, 12288), (16384, 16384), (32768, 8192),
+                         (65536, 65536), (20000, 20000)):
                 assert lib.svdj_dist_choose_block(code, world, m, n) == choose(dt, n // world, m), \
                     (dt, world, m, n)
 
