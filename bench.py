@@ -287,6 +287,7 @@ def run_native(a, dtype, work):
     from svdj.ops import kernels as K
     from svdj.parallel.comm import default_timeout_s, env_world
     from svdj.utils.metrics import algorithmic_flops_per_sweep, default_tol
+    from svdj.models.block import choose_mma
 
     rank, world, local = env_world()
     if world != a.gpus:
@@ -352,7 +353,8 @@ def run_native(a, dtype, work):
     p.W, p.m_pad, p.n_v, p.B = W, m_pad, n_v, B
     p.At, p.Vt, p.D = At.data_ptr(), Vt.data_ptr(), D.data_ptr()
     p.tol = a.tol if a.tol is not None else default_tol(dtype, m)
-    p.tol_mode, p.max_sweeps, p.mma = 0, a.max_sweeps, 0
+    mma = a.mma if a.mma != "auto" else choose_mma(dtype, W)
+    p.tol_mode, p.max_sweeps, p.mma = 0, a.max_sweeps, K.mma_code(mma, dtype)
     p.inner_order = {"cyclic": 0, "bipartite": 1, "cross": 2, "auto": 3}[a.inner_order]
     p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
     p.hist = C.cast(hist, C.POINTER(C.c_double))
@@ -429,7 +431,7 @@ def run_native(a, dtype, work):
                        "global_batch": 1, "seq_len": n,
                        "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
-                       "mma": "native", "precondition": "none", "chains": 2,
+                       "mma": mma, "precondition": "none", "chains": 2,
                        "inner_order": a.inner_order,
                        "exchange": a.exchange,
                        "staggered": bool(a.stagger), "root_owned": False},
@@ -488,8 +490,9 @@ def main():
     p.add_argument("--no-stagger", dest="stagger", action="store_false",
                    help="issue the two step chains independently (the default)")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
-                   help="block apply matrix cores (auto = native f32/f64 MFMA; bf16x6/bf16x3 "
-                        "split modes are faster but not fp32-accurate on every input)")
+                   help="block apply matrix cores (auto = bf16x6 for fp32 W=64 steps, f32/f64 "
+                        "MFMA otherwise; bf16x6 = 3-way bf16 split at fp32 accuracy, bf16x3 = "
+                        "2-way split, ~2^-17)")
     p.add_argument("--root-owned", action="store_true",
                    help="A on rank 0 before timing; scatter + gather of U,S,V timed")
     p.add_argument("--progress", action="store_true", help="one line per sweep on stderr")

@@ -108,10 +108,15 @@ class SolverConfig:
         """The dtype whose accuracy the stop test targets."""
         return torch.bfloat16 if self.bf16_mode(A) else self.resolved_dtype(A)
 
-    def resolved_mma(self, A: torch.Tensor | None) -> str:
+    def resolved_mma(self, A: torch.Tensor | None, W: int | None = None) -> str:
+        """Matrix-core mode of the block apply: "auto" is bf16x3 in the bf16
+        problem mode, else models.block.choose_mma(dtype, W)."""
         if self.mma != "auto":
             return self.mma
-        return "bf16x3" if self.bf16_mode(A) else "native"
+        if self.bf16_mode(A):
+            return "bf16x3"
+        from .models.block import choose_mma
+        return choose_mma(self.resolved_dtype(A), W or 0)
 
     def to_dict(self) -> dict:
         d = asdict(self)

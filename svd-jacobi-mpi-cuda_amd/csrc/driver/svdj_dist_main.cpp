@@ -5,7 +5,7 @@
 //
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
-//                  [--abs-tol] [--mma native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
+//                  [--abs-tol] [--mma auto|native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
 //                  [--exchange auto|direct|spread] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH] [--comm-timing] [--inject-fault RANK:SWEEP] [--keep-going]
@@ -162,7 +162,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.tol = tol;
   p.tol_mode = o.abs_tol ? 1 : 0;
   p.max_sweeps = o.max_sweeps;
-  p.mma = o.mma;
+  p.mma = o.mma < 0 ? svdj_choose_mma(dtype, W) : o.mma;
   p.inner_order = o.inner;
   p.exchange = o.exchange;
   p.stream_a = sa;
@@ -350,7 +350,7 @@ int main(int argc, char** argv) {
   }
   Opts o;
   o.n = std::atoi(argv[1]);
-  std::string mma = "native";
+  std::string mma = "auto";
   for (int i = 2; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -399,7 +399,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "N >= 1 and m >= N required\n");
     return 1;
   }
-  if (o.f32) o.mma = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
+  // -1 = auto: svdj_choose_mma once the block width is known (run_rank)
+  if (o.f32) o.mma = mma == "auto" ? -1 : (mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0));
 
   const char* env_rank = std::getenv("RANK");
   const char* env_world = std::getenv("WORLD_SIZE");

@@ -5,7 +5,7 @@
 //
 //   svdj_main N [--m M] [--input triu|dense] [--seed S] [--dtype f32|f64]
 //               [--method block|scalar] [--block W (default: by size)] [--max-sweeps K]
-//               [--tol T] [--mma native|bf16x6|bf16x3] [--inner cyclic|bipartite]
+//               [--tol T] [--mma auto|native|bf16x6|bf16x3] [--inner cyclic|bipartite]
 //               [--verify] [--report-dir DIR]
 //
 // Prints the reference's lines ("Dimensions, height: .., width: ..",
@@ -148,7 +148,7 @@ int main(int argc, char** argv) {
   unsigned seed = 1000000;
   double tol = -1;
   bool verify = false;
-  std::string input = "triu", dtype = "f64", method = "block", report_dir = ".", mma = "native";
+  std::string input = "triu", dtype = "f64", method = "block", report_dir = ".", mma = "auto";
   for (int i = 2; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -180,9 +180,10 @@ int main(int argc, char** argv) {
     svdj_ref_dense_input(m, n, A.data(), m, seed);
   else
     svdj_ref_triu_input(m, n, A.data(), m, seed);
-  const int mma_code = mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0);
   if (W == 0)  // models/block.py choose_block
     W = dtype == "f32" ? (n >= 1024 ? 64 : 32) : ((m >= 6144 && n >= 2048) ? 64 : 32);
+  const int mma_code = mma == "auto" ? svdj_choose_mma(dtype == "f32" ? 0 : 1, W)
+                                     : (mma == "bf16x6" ? 1 : (mma == "bf16x3" ? 2 : 0));
   if (dtype == "f32")
     return run<float>(m, n, A, method, W, max_sweeps, tol, mma_code, inner_order, verify, report_dir);
   return run<double>(m, n, A, method, W, max_sweeps, tol, 0, inner_order, verify, report_dir);

@@ -1507,17 +1507,37 @@ __device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&q)[NP], const bf16x8
   return acc;
 }
 
+// Waves own OUTPUT COLUMN tiles, not rows: wave w computes the 32 output
+// columns ct = w % NCT of the row tile (row group w / NCT; W = 64: all four
+// waves on one 32-row tile, W = 32: two 32-row tiles), so its split Q - I
+// fragments (NKB x NP bf16x8, 96 VGPRs for W = 64) stay in registers for
+// the whole workgroup.  The X tile is loaded once: wave w loads and splits
+// the k columns of its own output tile (k blocks 2ct, 2ct+1) into an LDS
+// image in B-fragment order (double-buffered, one barrier per tile), and
+// keeps those raw fp32 values for the epilogue Y = X + X (Q - I), where a
+// v_permlane32_swap moves them from the B-operand lanes to the accumulator
+// lanes.  No operand is re-read from global memory.
+//
+// Delta form (Q - I): the identity part is never rounded inside the
+// MFMA.  The bf16 MFMA's internal accumulation is not IEEE round-to-nearest,
+// and with X Q directly a dominant diagonal term biased every sum (column
+// norms drifted 780 eps in 400 near-identity applies, round 1); with the
+// identity added back in fp32 the drift is 0.14-0.17 eps against 3 eps for
+// the f32 MFMA (tools/probe_apply.py, profiles/r3_s3/bf16x6).
 template <int W, int NP>
 __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
     float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
     int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
     const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
   constexpr int N = 2 * W;
-  constexpr int NCT = N / 32;  // output column tiles
-  constexpr int NKB = N / 16;  // 16-deep k blocks
+  constexpr int NCT = N / 32;                   // output column tiles
+  constexpr int NKB = N / 16;                   // 16-deep k blocks
   constexpr int WAVES = kApplyThreads / SVDJ_WAVE;
+  constexpr int RG = WAVES / NCT;               // 32-row groups per tile
+  constexpr int TR = 32 * RG;                   // rows per tile
+  static_assert(NCT * RG == WAVES && NKB == 2 * NCT, "wave <-> (column tile, row group)");
   static_assert(W % 16 == 0, "k blocks must not straddle the two column blocks");
-  __shared__ bf16x8 Qf[NP][NCT][NKB][SVDJ_WAVE];
+  __shared__ bf16x8 Xf[2][RG][NKB][NP][SVDJ_WAVE];
 
   const int pair = blockIdx.x;
   if (skip[pair]) return;
@@ -1537,81 +1557,98 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
     r_begin = chunk * rows_v;
     r_end = min(n_v, r_begin + rows_v);
   }
-  // Q (row-major N x N, fp32) -> split A-operand fragments:
-  // fragment (ct, kb, lane l) = Q[kb*16 + 8(l>>5) + e][ct*32 + (l&31)], e = 0..7
-  const float* Qg = Qall + (size_t)pair * N * N;
-  for (int f = threadIdx.x; f < NCT * NKB * SVDJ_WAVE; f += kApplyThreads) {
-    const int l = f & 63, kb = (f >> 6) % NKB, ct = (f >> 6) / NKB;
-    const int j = ct * 32 + (l & 31), k0 = kb * 16 + 8 * (l >> 5);
-    bf16x8 parts[NP];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      __bf16 p[NP];
-      split_bf16<NP>(Qg[(k0 + e) * N + j], p);
-#pragma unroll
-      for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NP; ++i) Qf[i][ct][kb][l] = parts[i];
-  }
-  __syncthreads();
-
+  if (r_begin >= r_end) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
+  const int ct = wave % NCT, rg = wave / NCT;
   float* const xi = base + (size_t)bi * W * ld;
   float* const xj = base + (size_t)bj * W * ld;
-  // lane part of every address: column offset 8h, row c
-  const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
-  const uint32_t st_off = (uint32_t)(4 * h * ld + c);
-  auto load_tile = [&](float (&x)[NKB][8], int r) {
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-      const float* src = kb * 16 < W ? xi + (size_t)(kb * 16) * ld : xj + (size_t)(kb * 16 - W) * ld;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x[kb][e] = src[(size_t)e * ld + (lane_off + (uint32_t)r)];
-    }
-  };
-  int r0 = r_begin + wave * 32;
-  if (r0 >= r_end) return;
-  float xr[NKB][8];
-  load_tile(xr, r0);
-  while (true) {
-    const int rn = r0 + WAVES * 32;
-    const bool more = rn < r_end;
-    bf16x8 xs[NKB][NP];
+  // the wave's own 32 columns (k blocks 2ct, 2ct+1 = output tile ct)
+  float* const own = ct * 32 < W ? xi + (size_t)(ct * 32) * ld : xj + (size_t)(ct * 32 - W) * ld;
+
+  // Q - I fragments of column tile ct: (kb, lane) = Q[kb*16 + 8h + e][ct*32 + c] - delta
+  bf16x8 qf[NKB][NP];
+  {
+    const float* Qg = Qall + (size_t)pair * N * N + ct * 32 + c;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
+        const int k = kb * 16 + 8 * h + e;
         __bf16 p[NP];
-        split_bf16<NP>(xr[kb][e], p);
+        split_bf16<NP>(Qg[(size_t)k * N] - (k == ct * 32 + c ? 1.0f : 0.0f), p);
 #pragma unroll
-        for (int i = 0; i < NP; ++i) xs[kb][i][e] = p[i];
+        for (int i = 0; i < NP; ++i) qf[kb][i][e] = p[i];
       }
-    if (more) load_tile(xr, rn);  // next tile in flight during this tile's MFMAs
-    // Re-read the Q fragments from LDS per row tile: hoisted out of the loop
-    // they take 96-384 registers (W = 32/64) and force one wave per SIMD.
-    asm volatile("" ::: "memory");
+  }
+  // raw X of this wave's k blocks for rows r .. r+31: x[kbl][e] = X[r + c][ct*32 + 16 kbl + 8h + e]
+  const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
+  auto load = [&](float (&x)[2][8], int r) {
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
+    for (int kbl = 0; kbl < 2; ++kbl)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        x[kbl][e] = own[(size_t)(16 * kbl + e) * ld + (lane_off + (uint32_t)r)];
+  };
+  const uint32_t st_off = (uint32_t)(4 * h * ld + c);
+  int r0 = r_begin + rg * 32;  // this wave's rows in the current tile
+  float xr[2][8];
+  if (r0 < r_end) load(xr, r0);
+  // tile t covers rows r_begin + t TR .. + TR (the loop condition is uniform
+  // over the workgroup: every wave reaches every barrier)
+  for (int t = 0; r_begin + t * TR < r_end; ++t) {
+    const int buf = t & 1;
+    const bool mine = r0 < r_end;
+    // split this tile's own k blocks into the shared B-fragment image
+    if (mine) {
+#pragma unroll
+      for (int kbl = 0; kbl < 2; ++kbl) {
+        bf16x8 parts[NP];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 p[NP];
+          split_bf16<NP>(xr[kbl][e], p);
+#pragma unroll
+          for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) Xf[buf][rg][2 * ct + kbl][i][lane] = parts[i];
+      }
+    }
+    // epilogue operand: own raw values moved to accumulator lanes.  Output
+    // register g*4+i of lane (c, h) is column 8g + 4h + i of the tile; lane
+    // half h holds columns 16 kbl + 8h + e.
+    float xo[16];
+#pragma unroll
+    for (int kbl = 0; kbl < 2; ++kbl)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float keep = h ? xr[kbl][4 + i] : xr[kbl][i];
+        const float give = h ? xr[kbl][i] : xr[kbl][4 + i];
+        const float got = __int_as_float(half_swap(__float_as_int(give)));
+        xo[(2 * kbl) * 4 + i] = h ? got : keep;
+        xo[(2 * kbl + 1) * 4 + i] = h ? keep : got;
+      }
+    const int rn = r0 + TR;
+    if (rn < r_end) load(xr, rn);  // next tile in flight during this tile's MFMAs
+    __syncthreads();
+    if (mine) {
       f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        bf16x8 q[NP];
+        bf16x8 xs[NP];
 #pragma unroll
-        for (int i = 0; i < NP; ++i) q[i] = Qf[i][ct][kb][lane];
+        for (int i = 0; i < NP; ++i) xs[i] = Xf[buf][rg][kb][i][lane];
         // the high-order product in its own accumulator, the small terms in
-        // a second one (two chains remove the bias of a single chain)
-        lo = mfma_split<NP, 1>(q, xs[kb], lo);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[0], xs[kb][0], acc, 0, 0, 0);
+        // a second one
+        lo = mfma_split<NP, 1>(qf[kb], xs, lo);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
       }
       acc += lo;
-      float* dst = ct * 32 < W ? xi + (size_t)(ct * 32) * ld : xj + (size_t)(ct * 32 - W) * ld;
 #pragma unroll
       for (int e = 0; e < 16; ++e)
-        dst[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = acc[e];
+        own[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = xo[e] + acc[e];
     }
-    if (!more) break;
     r0 = rn;
   }
 }
@@ -1645,7 +1682,11 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // (mma != 0) keep 2048: their larger Q images (32768x8192 bf16 with QR:
   // 811 -> 847 ms at 512).
   int total_rows = m_pad + n_v;
-  const int wg_target = W == 64 && P < 64 && mma == 0 ? 512 : 2048;
+  // The split-bf16 apply (mma != 0, Q held in registers per output column
+  // tile) wants 2048 unless a step has few pairs: 1 GPU 8192^2 664 ms at
+  // 2048 vs 756 at 512, 16384^2 P=8 rank plan 52.3 vs 50.3 ms per sweep at
+  // 2048 vs 512 (profiles/r3_s3/bf16x6).
+  const int wg_target = mma == 0 ? (W == 64 && P < 64 ? 512 : 2048) : (P <= 16 ? 512 : 2048);
   int rows = round_up((int)(((long)total_rows * P + wg_target - 1) / wg_target), 128);
   if (rows < 128) rows = 128;
   if (rows > 2048) rows = 2048;
@@ -1798,11 +1839,11 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
 // mma: 0 = native matrix cores for the data type (f32 / f64 MFMA),
 //      1 = fp32 data on bf16 MFMA, 3-way split (fp32-level accuracy),
 //      2 = fp32 data on bf16 MFMA, 2-way split (~2^-17 accuracy, fast mode).
-// Measured (tools/probe_apply.py, bench.py accuracy check): the split modes
-// are as accurate as f32 MFMA on unstructured data, but the bf16 MFMA's
-// internal accumulation is biased when one 16-product group mixes magnitudes
-// (a dominant column, or Q ~ I late in the iteration): on U(0,1) 8192^2 the
-// final ||AV - US||/||A|| is 6.5e-4 vs 8e-6 native.  Native is the default.
+// Both split modes run in delta form, Y = X + X (Q - I) (apply_split_kernel).
+// Measured on MI355X (bench.py accuracy block, profiles/r3_s3/bf16x6): mode 1
+// matches the f32 MFMA path in residual, U/V orthogonality and sigma error at
+// 512..16384 and is 12-23 % faster per sweep for W = 64, so it is the fp32
+// default there (svdj_choose_mma).
 template <typename T, int W>
 static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inner,
                          uint32_t* metric, int mma) {
@@ -1899,6 +1940,12 @@ using namespace svdj;
 extern "C" int svdj_choose_inner_order(int W, int pairs) {
   return (W == 64 && pairs <= 16) ? 2 : 1;
 }
+
+// Default matrix-core mode ("auto") for data type `dtype` (0 fp32, 1 fp64)
+// and block width W (models/block.py choose_mma): the split-bf16 apply for
+// fp32 W = 64; W = 32 steps stay on f32 MFMA (4096^2 P=8
+// rank plan, W = 32: 8.55 vs 9.61 ms per sweep with the split).
+extern "C" int svdj_choose_mma(int dtype, int W) { return (dtype == 0 && W == 64) ? 1 : 0; }
 
 extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
   return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);

@@ -69,11 +69,15 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   mma     matrix-core mode: 0 native (f32 / f64 MFMA), 1 fp32 data on bf16
 //           MFMA with a 3-way bf16 split (6 products, fp32-level accuracy),
 //           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
+//           Both split modes apply Y = X + X (Q - I), the identity in fp32.
 // Workspace size for one step: svdj_block_workspace_bytes().
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
 // inner_order code (1 bipartite, 2 cross-only) for steps of `pairs` pairs of
 // W-wide blocks: models/block.py choose_inner_order.
 int svdj_choose_inner_order(int W, int pairs);
+// Default ("auto") matrix-core mode for dtype (0 fp32, 1 fp64) and block width
+// W: 1 (split bf16) for fp32 W = 64, else 0 (models/block.py choose_mma).
+int svdj_choose_mma(int dtype, int W);
 int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, const int32_t* pairs, int P,
                      int steps, const int32_t* modes, double tol, int tol_mode,

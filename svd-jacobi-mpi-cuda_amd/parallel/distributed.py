@@ -35,7 +35,7 @@ import torch
 from ..config import SolverConfig, SVDOptions
 from ..models.base import SVDResult, Solver
 from ..models import precondition as pre
-from ..models.block import choose_block, resolve_inner_order
+from ..models.block import choose_block, choose_mma, resolve_inner_order
 from ..ops import kernels as K
 from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
@@ -226,9 +226,9 @@ class DistributedBlockJacobi(Solver):
         dev = comm.device
         dtype = torch.float64 if pdtype == torch.float64 else torch.float32
         bf16 = pdtype == torch.bfloat16
-        mma = cfg.mma if cfg.mma != "auto" else ("bf16x3" if bf16 else "native")
         geo = self.geometry(m, n, dtype)
         P, W, B, k, m_pad, n_v, ncols = (geo[x] for x in ("P", "W", "B", "k", "m_pad", "n_v", "ncols"))
+        mma = cfg.mma if cfg.mma != "auto" else ("bf16x3" if bf16 else choose_mma(dtype, W))
         g = comm.rank
         tour = tournament(P)
         pipelined = cfg.chains == 2

@@ -213,3 +213,21 @@ def test_native_inner_order_rule_matches_python():
     for W in (32, 64):
         for pairs in (1, 4, 8, 16, 17, 32, 64, 128, 256):
             assert code[lib.svdj_choose_inner_order(W, pairs)] == choose(W, pairs), (W, pairs)
+
+
+def test_native_mma_rule_matches_python():
+    """mma="auto": the native drivers and engine (svdj_choose_mma in
+    libsvdj_hip) pick the apply's matrix-core mode by the same rule as
+    models.block.choose_mma / SolverConfig.resolved_mma."""
+    import torch
+    choose = svdj.models.block.choose_mma
+    lib = svdj.ops.hip_lib()
+    code = {0: "native", 1: "bf16x6"}
+    for dt, dcode in ((torch.float32, 0), (torch.float64, 1)):
+        for W in (32, 64):
+            assert code[lib.svdj_choose_mma(dcode, W)] == choose(dt, W), (dt, W)
+    cfg = svdj.SolverConfig()
+    A = torch.zeros(4, 4, dtype=torch.float32)
+    assert cfg.resolved_mma(A, 64) == "bf16x6" and cfg.resolved_mma(A, 32) == "native"
+    assert cfg.resolved_mma(A.double(), 64) == "native"
+    assert svdj.SolverConfig(mma="native").resolved_mma(A, 64) == "native"
