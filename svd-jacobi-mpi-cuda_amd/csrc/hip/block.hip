@@ -1153,24 +1153,31 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
   T h2src = T(0);           // E_t[a+1][a-1] (lane a-1's E_t[(a-1)+2][a-1])
   T dx_out = T(0), dy_out = T(0);
   Q2* rq = rec + (size_t)pair * (kCrossMaxInner * W) * W;
-  auto solve = [&](T dx, T dy, T g, int step, bool& rot) {
+  T rt = T(0);  // tangent of the latest solved rotation; its fp64 record is
+                // written at the start of the next phase (steps 0 .. gs-1 are
+                // recorded; the look-ahead rotation solved in the final phase
+                // is never used)
+  auto solve = [&](T dx, T dy, T g, bool& rot) {
     T c, sn, t;
     rot = rotation_fast(dx, dy, g, tol, absmode, nfloor, c, sn, t);
+    rc = c;
+    rs = sn;
+    rt = t;
+    rdx = dx - t * g;
+    rdy = dy + t * g;
+    pend = rot ? T(0) : g;
+  };
+  auto record = [&](int step) {
     double c64, s64;
     if constexpr (sizeof(T) == 8) {
-      c64 = c;
-      s64 = sn;
+      c64 = rc;
+      s64 = rs;
     } else {  // fp64 (c, s) of the fp32 t, normalised in fp64 (Q stays orthogonal)
-      const double td = (double)t;
+      const double td = (double)rt;
       c64 = rsqrt64(fma(td, td, 1.0));
       s64 = td * c64;
     }
     if (step < kCrossMaxInner * W) rq[(size_t)step * W + a] = Q2{c64, s64};
-    rc = c;
-    rs = sn;
-    rdx = dx - t * g;
-    rdy = dy + t * g;
-    pend = rot ? T(0) : g;
   };
   int racc = 0, racc_next = 0;
   if (run && solver) {  // step 0 of slot a
@@ -1178,7 +1185,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     h2src = Eb[0][((a + 1) % W) * W + (a + W - 1) % W];
     g1 = Eb[0][a * W + (a + 1) % W];
     bool rot;
-    solve(dg[a], dg[W + a], Eb[0][a * W + a], 0, rot);
+    solve(dg[a], dg[W + a], Eb[0][a * W + a], rot);
     racc = rot;
     rcs[0][a] = T2{rc, rs};
   }
@@ -1192,6 +1199,9 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     if (wave == 0) {
       // neighbours' values (slot a+1, a+2) by lane rotates; E_t[a][a+2] from LDS
       const T g2 = solver ? Eb[b][a * W + (a + 2) % W] : T(0);
+      // fp64 record of step gs (solved in the previous phase) while the LDS
+      // read is in flight: off the barrier-to-barrier critical path
+      if (solver) record(gs);
       const T c1 = bip_shift<W>(rc, a), s1 = bip_shift<W>(rs, a);
       const T c2 = bip_shift<W>(c1, a), s2 = bip_shift<W>(s1, a);
       const T h1 = bip_shift<W>(pend_prev, a);  // E_t[a+1][a]
@@ -1210,7 +1220,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
         g1 = n0_2;
         h2src = n1_1;
         bool rot;
-        solve(rdx, dyn, n0_1, gs + 1, rot);
+        solve(rdx, dyn, n0_1, rot);
         if (last) racc_next |= rot; else racc |= rot;
         rcs[nb][a] = T2{rc, rs};
       }
