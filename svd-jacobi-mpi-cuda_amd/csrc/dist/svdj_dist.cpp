@@ -551,7 +551,7 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
     if (r < 0 && !rc) rc = r;
   };
   // 3 = auto: by the pairs of a cross step (half super-blocks)
-  const int io = p->inner_order == 3 ? svdj_choose_inner_order(W, h->hk) : p->inner_order;
+  const int io = p->inner_order == 3 ? svdj_choose_inner_order(p->dtype, W, h->hk) : p->inner_order;
   guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
   for (int c = 0; c < 2 && !rc; ++c)

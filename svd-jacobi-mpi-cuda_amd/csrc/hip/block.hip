@@ -1945,10 +1945,12 @@ using namespace svdj;
 
 // Cross-step EVD ordering for a step of `pairs` pairs of W-wide blocks
 // (models/block.py choose_inner_order, measurements there): 2 = cross-only
-// (low-latency EVD + row-parallel Q build) for few W = 64 pairs, else 1 =
-// bipartite.  The inner_order codes of svdj_block_solve / svdj_dist_problem.
-extern "C" int svdj_choose_inner_order(int W, int pairs) {
-  return (W == 64 && pairs <= 16) ? 2 : 1;
+// (low-latency EVD + row-parallel Q build) for fp32 W = 64 and for fp64
+// W = 64 with more than 16 pairs, else 1 = bipartite.  The inner_order codes
+// of svdj_block_solve / svdj_dist_problem.
+extern "C" int svdj_choose_inner_order(int dtype, int W, int pairs) {
+  if (W != 64) return 1;
+  return (dtype == 0 || pairs > 16) ? 2 : 1;
 }
 
 // Default matrix-core mode ("auto") for data type `dtype` (0 fp32, 1 fp64)
@@ -2072,7 +2074,7 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
       o[2 * k + 1] = a < b ? b : a;
     }
   }
-  if (inner_order == 3) inner_order = svdj_choose_inner_order(W, P);  // auto
+  if (inner_order == 3) inner_order = svdj_choose_inner_order(dtype, W, P);  // auto
   if (inner_order < 0 || inner_order > 2) {
     set_error("inner_order %d (0 cyclic, 1 bipartite, 2 cross, 3 auto)", inner_order);
     return -2;

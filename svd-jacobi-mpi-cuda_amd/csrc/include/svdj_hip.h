@@ -73,8 +73,9 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 // Workspace size for one step: svdj_block_workspace_bytes().
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
 // inner_order code (1 bipartite, 2 cross-only) for steps of `pairs` pairs of
-// W-wide blocks: models/block.py choose_inner_order.
-int svdj_choose_inner_order(int W, int pairs);
+// W-wide blocks of data type `dtype` (0 fp32, 1 fp64): models/block.py
+// choose_inner_order.
+int svdj_choose_inner_order(int dtype, int W, int pairs);
 // Default ("auto") matrix-core mode for dtype (0 fp32, 1 fp64) and block width
 // W: 1 (split bf16) for fp32 W = 64, else 0 (models/block.py choose_mma).
 int svdj_choose_mma(int dtype, int W);

@@ -21,8 +21,8 @@ def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
 
     W=64 halves the steps and the per-byte traffic of the Gram and the apply,
     but its EVD is slower and a step holds half as many pairs.  Since the
-    low-latency cross EVD (choose_inner_order "cross" for <= 16 W=64 pairs
-    per step, round 3) the W=64 EVD no longer dominates small problems, and
+    low-latency cross EVD (choose_inner_order "cross" for W=64 steps,
+    round 3) the W=64 EVD no longer dominates small problems, and
     W=64 wins almost everywhere.  Measured on MI355X, round 3
     (profiles/r3_blockw), W=32 / W=64:
       * fp32, 1 GPU n x n, ms per solve: 512 15.7 / 12.1, 1024 21.5 / 21.1,
@@ -42,20 +42,25 @@ def choose_block(dtype: torch.dtype, n: int, m: int) -> int:
     return 64 if n >= 1024 else 32
 
 
-def choose_inner_order(W: int, pairs_per_step: int) -> str:
+def choose_inner_order(W: int, pairs_per_step: int, dtype: torch.dtype = torch.float32) -> str:
     """EVD ordering of the cross steps for ``pairs_per_step`` pairs of W-wide
     blocks per step (config inner_order="auto").
 
     "cross" (evd_cross_kernel + qbuild_kernel: a low-latency EVD that
     tracks only the cross couplings, Q built row-parallel by a second kernel)
-    when a step has few W=64 pairs and the EVD latency is on the critical
-    path; "bipartite" (one workgroup per pair, Q in registers) otherwise,
-    where the EVD hides under the other chain and its total CU time counts.
-    Measured on MI355X, 16384^2 fp32 rank plans, ms per sweep
-    bipartite / cross: P=8 (8 pairs) 59.1 / 51.0, P=4 (16) 112.5 / 108.1,
-    P=2 (32) 201.5 / 202.4; 1 GPU (64 pairs) 5.78 / 5.87 s per solve;
-    8192^2 P=8 (W=32) 20.0 / 22.1 (profiles/r3_evd)."""
-    return "cross" if (W == 64 and pairs_per_step <= 16) else "bipartite"
+    for fp32 W=64 steps and fp64 W=64 steps with more than 16 pairs;
+    "bipartite" (one workgroup per pair, Q in registers) otherwise.  Measured on MI355X, 16384^2 fp32 rank plans, ms per sweep
+    bipartite / cross, with the f32-MFMA apply (profiles/r3_evd): P=8 (8
+    pairs) 59.1 / 51.0, P=4 (16) 112.5 / 108.1, P=2 (32) 201.5 / 202.4; with
+    the split-bf16 apply, whose shorter steps expose the EVD more
+    (profiles/r3_s3/inner): P=2 177.0 / 171.0, 1 GPU (64 pairs) 341.2 /
+    341.1; 8192^2 P=2 27.8 / 25.7.  W=32: 8192^2 P=8 20.0 / 22.1.  fp64 (f64-MFMA
+    apply, larger LDS image in the cross EVD): 16384^2 P=8 (16 pairs) 127.8 /
+    140.3, 10000^2 P=2 (20 pairs) 126.0 / 121.4, 10000^2 1 GPU (39 pairs) 184 /
+    175 ms per sweep."""
+    if W != 64:
+        return "bipartite"
+    return "cross" if (dtype != torch.float64 or pairs_per_step > 16) else "bipartite"
 
 
 def choose_mma(dtype: torch.dtype, W: int) -> str:
@@ -73,8 +78,9 @@ def choose_mma(dtype: torch.dtype, W: int) -> str:
     return "bf16x6" if (dtype == torch.float32 and W == 64) else "native"
 
 
-def resolve_inner_order(order: str, W: int, pairs_per_step: int) -> str:
-    return choose_inner_order(W, pairs_per_step) if order == "auto" else order
+def resolve_inner_order(order: str, W: int, pairs_per_step: int,
+                        dtype: torch.dtype = torch.float32) -> str:
+    return choose_inner_order(W, pairs_per_step, dtype) if order == "auto" else order
 
 
 class BlockJacobi(Solver):
@@ -102,7 +108,7 @@ class BlockJacobi(Solver):
         tol = self.tolerance(cfg.precision_dtype(A), m)
         with Timer(device) as tm:
             D = K.col_norms2(At, m_pad)
-            inner = resolve_inner_order(cfg.inner_order, W, ncols // (2 * W))
+            inner = resolve_inner_order(cfg.inner_order, W, ncols // (2 * W), dtype)
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
                                          cfg.max_sweeps, mma=mma, tol_mode=cfg.tol_mode,
                                          inner_order=inner)

@@ -107,7 +107,7 @@ def hip_lib():
              [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
               c_double, c_int, c_int, c_void_p, c_f64_p, c_void_p])
         _sig(lib, "svdj_block_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int])
-        _sig(lib, "svdj_choose_inner_order", c_int, [c_int, c_int])
+        _sig(lib, "svdj_choose_inner_order", c_int, [c_int, c_int, c_int])
         _sig(lib, "svdj_block_steps", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
               c_int, c_int, c_i32_p, c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_int,

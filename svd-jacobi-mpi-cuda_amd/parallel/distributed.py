@@ -258,7 +258,7 @@ class DistributedBlockJacobi(Solver):
         D = K.col_norms2(At, m_pad)
         tol = self.tolerance(pdtype, m)
         # pairs per cross step: half super-blocks (pipelined) or whole ones
-        inner = resolve_inner_order(cfg.inner_order, W, k // 2 if pipelined else k)
+        inner = resolve_inner_order(cfg.inner_order, W, k // 2 if pipelined else k, dtype)
         if pipelined:
             rA = rV = rD = None
         else:  # blocking exchange (chains=1) receives into a staging block

@@ -207,12 +207,15 @@ def test_native_inner_order_rule_matches_python():
     """inner_order="auto": the native drivers (svdj_choose_inner_order in
     libsvdj_hip) pick the cross-step EVD by the same rule as
     models.block.choose_inner_order."""
+    import torch
     choose = svdj.models.block.choose_inner_order
     lib = svdj.ops.hip_lib()
     code = {1: "bipartite", 2: "cross"}
-    for W in (32, 64):
-        for pairs in (1, 4, 8, 16, 17, 32, 64, 128, 256):
-            assert code[lib.svdj_choose_inner_order(W, pairs)] == choose(W, pairs), (W, pairs)
+    for dt, dcode in ((torch.float32, 0), (torch.float64, 1)):
+        for W in (32, 64):
+            for pairs in (1, 4, 8, 16, 17, 32, 64, 128, 256):
+                assert code[lib.svdj_choose_inner_order(dcode, W, pairs)] == choose(W, pairs, dt), \
+                    (dt, W, pairs)
 
 
 def test_native_mma_rule_matches_python():
