@@ -37,6 +37,16 @@ import time
 
 import torch
 
+# What each matrix-core mode of the block apply computes (reported in the JSON line).
+MMA_NUMERICS = {
+    "native": "IEEE f32/f64 MFMA products and sums",
+    "bf16x6": ("fp32 data, fp32 accumulation: every fp32 operand split exactly into 3 RNE bf16 "
+               "parts, the 6 products of order < 3 on bf16 MFMA (dropped terms < 2^-26 relative), "
+               "delta form X + X(Q - I) with the identity added in fp32; accuracy block = the "
+               "check (README 'Matrix-core modes')"),
+    "bf16x3": "bf16 problem mode: 2-way bf16 split (~2^-17), fp32 master copies",
+}
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -431,7 +441,8 @@ def run_native(a, dtype, work):
                        "global_batch": 1, "seq_len": n,
                        "parallelism": f"colblock{a.gpus} (2 super-blocks/GPU, RCCL tournament)",
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
-                       "mma": mma, "precondition": "none", "chains": 2,
+                       "mma": mma, "mma_numerics": MMA_NUMERICS.get(mma, ""),
+                       "precondition": "none", "chains": 2,
                        "inner_order": a.inner_order,
                        "exchange": a.exchange,
                        "staggered": bool(a.stagger), "root_owned": False},
@@ -640,6 +651,7 @@ def main():
                 "block_W": geo["W"],
                 "super_block_B": geo["B"],
                 "mma": last.info.get("mma", a.mma),
+                "mma_numerics": MMA_NUMERICS.get(last.info.get("mma", a.mma), ""),
                 "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
                 "inner_order": last.info.get("inner_order", a.inner_order),
