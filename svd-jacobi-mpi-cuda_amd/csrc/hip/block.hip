@@ -1799,7 +1799,10 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int RL = W == 64 ? 16 : 8;  // one workgroup per pair
-    if (c.P >= 32)
+    // 16 rows per lane from 64 pairs per step; at 32 pairs 4 rows per lane is
+    // faster (1 GPU 8192^2 709 -> 672 ms, 16384^2 P=2 plan 171.4 -> 169.1 ms per
+    // sweep; 1 GPU 16384^2 (64 pairs) equal at 4/8/16, profiles/r3_s3/qbuild)
+    if (c.P >= 64)
       hipLaunchKernelGGL((qbuild_kernel<T, W, RL>), dim3(c.P, qbuild_blocks<W, RL>()),
                          dim3(kQbThreads), 0, c.st, c.rec, c.nsteps, c.skipb[b], c.Qb[b]);
     else
