@@ -1675,7 +1675,10 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // Many pairs per step want few chunks (every chunk is a slab the EVD sums:
   // 1-GPU 16384^2, W=64, 5.92 s at 512 vs 6.23 s at 2048).  With few pairs
   // (many GPUs) 64-256 measured slower (8-GPU rank plan 65.5 -> 74-78 ms).
-  constexpr int gram_target = 512;
+  // With the split-bf16 apply, steps of >= 32 pairs want ~256 (1 GPU 16384^2
+  // 4.94 -> 4.84 s, 8192^2 674 -> 659 ms, P=2 plan 165.8 -> 163.5 ms per sweep);
+  // the P=4 plan (16 pairs) is 6 % slower at 256 (profiles/r3_s3/gram).
+  const int gram_target = P >= 32 ? 256 : 512;
   int want = (gram_target + P - 1) / P;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
