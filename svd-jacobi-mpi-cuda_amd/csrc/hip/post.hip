@@ -99,7 +99,7 @@ extern "C" int svdj_spin_ns(double ns, void* stream) {
 extern "C" const char* svdj_hip_last_error(void) { return g_err; }
 
 extern "C" const char* svdj_hip_version(void) {
-  return "svdj-hip 0.1 gfx950 (mfma_f32_32x32x2f32, mfma_f64_16x16x4f64)";
+  return "svdj-hip 0.1 gfx950 (mfma_f32_32x32x2f32, mfma_f32_32x32x16_bf16 split-fp32, mfma_f64_16x16x4f64)";
 }
 
 extern "C" int svdj_set_identity(int dtype, void* V, int n_v, int ldv, int ncols, int col_offset,
