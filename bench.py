@@ -240,7 +240,8 @@ def simulate(a, cfg, dtype, work):
         "solve_s": round(el, 4), "dtype": a.dtype,
         "config": {"model": f"{m}x{n} {a.dtype}", "block_W": geo["W"], "super_block_B": geo["B"],
                    "chains": a.chains, "inner_order": res.info.get("inner_order", a.inner_order),
-                   "link_gbps_model": a.sim_link_gbps, "exchange": comm.exchange},
+                   "link_gbps_model": a.sim_link_gbps, "exchange": comm.exchange,
+                   "quad_steps": bool(res.info.get("quad", False))},
         "comm": res.info.get("comm"),
         "qr_seconds": res.info.get("qr_seconds"),
         "sim_bytes_per_exchange": comm.bytes_moved // max(comm.exchanges, 1),
@@ -518,6 +519,8 @@ def main():
     p.add_argument("--exchange", default="auto", choices=["auto", "direct", "spread"],
                    help="half super-block transfer: one link (direct) or all links, relayed "
                         "(spread); auto = spread from 4 GPUs")
+    p.add_argument("--quad", default="auto", choices=["auto", "on", "off"],
+                   help="fused two-step quad block steps (fp32 W=64 split-bf16; auto: off)")
     p.add_argument("--simulate-P", type=int, default=0)
     p.add_argument("--simulate-rank", type=int, default=0)
     p.add_argument("--sim-sweeps", type=int, default=3)
@@ -544,7 +547,8 @@ def main():
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
                             stagger=bool(a.stagger), precondition=a.precondition,
                             inner_order=a.inner_order,
-                            progress=a.progress, comm_timing=a.comm_timing, exchange=a.exchange)
+                            progress=a.progress, comm_timing=a.comm_timing, exchange=a.exchange,
+                            quad=a.quad)
     if a.inject_fault:
         r_, s_ = (int(x) for x in a.inject_fault.split(":"))
         cfg.extra["fault_exit"] = (r_, s_)
@@ -658,6 +662,7 @@ def main():
                 "staggered": bool(a.stagger),
                 "root_owned": a.root_owned,
                 "exchange": last.info.get("exchange", a.exchange),
+                "quad_steps": bool(last.info.get("quad", False)),
             },
             "sweeps": sweeps,
             "converged": conv,

@@ -76,6 +76,10 @@ class SolverConfig:
     # chunks, relayed over all links in two phases (parallel/spread.py);
     # auto: spread from 4 GPUs up
     exchange: str = "auto"
+    # distributed, pipelined: fuse cross steps two at a time over quads of
+    # blocks (csrc/hip/block.hip "quad step": Gram-space second-step
+    # couplings, one K = 256 apply per two steps).  auto: models.block.choose_quad
+    quad: str = "auto"
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
@@ -88,6 +92,8 @@ class SolverConfig:
             raise ValueError("max_sweeps / max_inner_sweeps must be >= 0")
         if self.exchange not in ("auto", "direct", "spread"):
             raise ValueError(f"exchange must be auto, direct or spread, got {self.exchange!r}")
+        if self.quad not in ("auto", "on", "off"):
+            raise ValueError(f"quad must be auto, on or off, got {self.quad!r}")
 
     def bf16_mode(self, A: torch.Tensor | None = None) -> bool:
         """bf16 problem: bf16 in/out, fp32 master copies of A and V, block
@@ -142,6 +148,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--progress", action="store_true", help="print one line per sweep (rank 0)")
+    p.add_argument("--quad", default="auto", choices=["auto", "on", "off"],
+                   help="fused two-step quad block steps (fp32, W=64, split-bf16 apply)")
     return p
 
 
@@ -152,5 +160,6 @@ def config_from_args(a) -> SolverConfig:
                         mma=a.mma, precondition=a.precondition, checkpoint_dir=a.checkpoint_dir,
                         checkpoint_every=a.checkpoint_every,
                         progress=bool(getattr(a, "progress", False)),
+                        quad=getattr(a, "quad", "auto"),
                         **({"inner_order": a.inner_order}
                            if getattr(a, "inner_order", None) else {}))

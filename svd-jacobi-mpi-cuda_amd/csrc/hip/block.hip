@@ -48,7 +48,31 @@ __host__ __device__ constexpr int round_up(int a, int b) { return (a + b - 1) / 
 // For fp64 W = 64 the cross products are also split over blockIdx.z in XS = 2
 // row halves (x tiles), so accumulators plus the double-buffered loads fit in
 // registers without spilling.
-enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2 };
+//       GRAM_QUAD   the cross Grams a quad step needs (see "quad step" below):
+//                   `pairs` holds two steps (s: (a,c),(b,d); s+1: (a,d),(b,c)
+//                   per quad), gridDim.x = 3P: slabs [0, P) are step s's
+//                   pairs, slab P + 4q + r the blocks (a,d), (b,c), (a,b),
+//                   (c,d) of quad q.
+enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2, GRAM_QUAD = 3 };
+
+// (bi, bj) of Gram slab `pair` (see GRAM_QUAD).
+template <int MODE>
+__device__ __forceinline__ void gram_pair(const int32_t* __restrict__ pairs, int pair, int& pi,
+                                          int& pj) {
+  if constexpr (MODE == GRAM_QUAD) {
+    const int P = (int)gridDim.x / 3;
+    if (pair >= P) {
+      const int j = pair - P, q = j >> 2, r = j & 3;
+      const int32_t* s0 = pairs + 4 * q;          // (a, c), (b, d)
+      const int32_t* s1 = pairs + 2 * P + 4 * q;  // (a, d), (b, c)
+      pi = r == 0 ? s1[0] : r == 1 ? s1[2] : r == 2 ? s0[0] : s0[1];
+      pj = r == 0 ? s1[1] : r == 1 ? s1[3] : r == 2 ? s0[2] : s0[3];
+      return;
+    }
+  }
+  pi = pairs[2 * pair];
+  pj = pairs[2 * pair + 1];
+}
 template <typename T, int W>
 __host__ __device__ constexpr int gram_xsplit() { return (sizeof(T) == 8 && W == 64) ? 2 : 1; }
 
@@ -93,7 +117,8 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
   const int region = MODE == GRAM_SPLIT ? (int)blockIdx.z / XS : 2;
   const int xpart = FULL ? 0 : (int)blockIdx.z % XS;
-  const int pi = pairs[2 * pair], pj = pairs[2 * pair + 1];
+  int pi, pj;
+  gram_pair<MODE>(pairs, pair, pi, pj);
   const int bi = region == 1 ? pj : pi, bj = region == 0 ? pi : pj;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r_begin = chunk * rows_per_chunk;
@@ -1663,11 +1688,397 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
   }
 }
 
+// ------------------------------------------------------------- quad step
+// Two consecutive cross steps fused (fp32, W = 64, split-bf16 apply).  Four
+// W-blocks (a, b, c, d) = the block pairs (a,c),(b,d) of step s and
+// (a,d),(b,c) of step s+1 (a super-block pair {a,b} x {c,d}, the schedule
+// of parallel/schedule.py quad_round_robin / quad_bipartite).  Step s+1's
+// couplings are formed in Gram space instead of from the data:
+//   gram   : the six cross Grams C_ac, C_bd, C_ad, C_bc, C_ab, C_cd in ONE
+//            launch (GRAM_QUAD; each block of the quad is read for three
+//            products instead of once per step);
+//   evd 1  : evd_cross_kernel on (a,c), (b,d)  -> rotation records;
+//   T1     : qbuild_quad_kernel<1> -> Q_ac, Q_bd in fp64;
+//   update : C(a',d') = [Q_aa;Q_ca]^T [[C_ab,C_ad],[C_cb,C_cd]] [Q_bd;Q_dd] and
+//            C(b',c') likewise (quad_update_kernel): exact in Gram space, the
+//            within-pair blocks C_ab, C_cd included;
+//   evd 2  : evd_cross_kernel on (a,d), (b,c) from those couplings;
+//   T      : qbuild_quad_kernel<2> applies the step-(s+1) rotations to the
+//            rows of T1 in fp64: T = T1 T2, the whole 256 x 256 transform;
+//   apply  : [a b c d] <- [a b c d] T once, for A and V (apply_quad_kernel).
+// The data moves through HBM once per two steps instead of twice, and the
+// apply contracts over K = 256 instead of 128: its split-bf16 MFMAs, no
+// longer waiting on HBM, set the pace.  Numerically it is the two W-block
+// steps with the same pairs (same EVDs, the couplings of step s+1 computed
+// from the exact rotations of step s), and T is accumulated in fp64 and
+// rounded once instead of twice.
+
+// Q of an EVD pair (phase 1, rows of the pair, output fp64 T1) or the quad's
+// T (phase 2: rows of all 4 blocks, starting from the phase-1 transforms,
+// output fp32).  Same row-parallel rotation loop as qbuild_kernel; a skipped
+// pair contributes the identity (phase 1 writes it: T1 is read by update and
+// phase 2 even when its pair did not rotate).
+template <int PHASE, int R>
+__global__ __launch_bounds__(kQbThreads) void qbuild_quad_kernel(
+    const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
+    const int32_t* __restrict__ skip, double* __restrict__ T1, float* __restrict__ Tq) {
+  constexpr int W = 64, N = 2 * W, QN = 4 * W;
+  constexpr int WAVES = kQbThreads / SVDJ_WAVE;
+  static_assert((PHASE == 1 ? N : QN) % (R * WAVES) == 0, "row cover");
+  using Q2 = Pair2<double>;
+  __shared__ Q2 rs[kQbChunk * W];
+  const int pair = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int a = lane;
+  const int k0 = (blockIdx.y * WAVES + wave) * R;
+  const int ns = skip[pair] ? 0 : nsteps[pair];
+  const Q2* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  const int q = pair >> 1, j = pair & 1;
+  double qx[R], qy[R];
+  if constexpr (PHASE == 1) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      qx[i] = (k0 + i == a) ? 1.0 : 0.0;
+      qy[i] = (k0 + i == W + a) ? 1.0 : 0.0;
+    }
+  } else {
+    // sub-pair j = 0: (a', d'), x = a' (column a of Q_ac), y = d' (column
+    // W + a of Q_bd); j = 1: (b', c'), x = b' (Q_bd), y = c' (Q_ac).  Quad
+    // row k is block k >> 6 in [a b c d] order: Q_ac holds rows of a, c (even
+    // blocks), Q_bd rows of b, d (odd blocks).
+    const double* tx = T1 + (size_t)(2 * q + j) * N * N;
+    const double* ty = T1 + (size_t)(2 * q + 1 - j) * N * N;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int k = k0 + i, rb = k >> 6, kl = ((rb >> 1) << 6) + (k & 63);
+      qx[i] = (rb & 1) == j ? tx[(size_t)kl * N + a] : 0.0;
+      qy[i] = (rb & 1) != j ? ty[(size_t)kl * N + W + a] : 0.0;
+    }
+  }
+  for (int t0 = 0; t0 < ns; t0 += kQbChunk) {
+    const int nc = ns - t0 < kQbChunk ? ns - t0 : kQbChunk;
+    for (int i = threadIdx.x; i < nc * W; i += kQbThreads) rs[i] = rp[(size_t)t0 * W + i];
+    __syncthreads();
+    Q2 n0 = rs[a], n1 = nc > 1 ? rs[W + a] : Q2{1.0, 0.0};
+    for (int t = 0; t < nc; ++t) {
+      const Q2 cs = n0;
+      n0 = n1;
+      if (t + 2 < nc) n1 = rs[(t + 2) * W + a];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const double x = qx[i], y = qy[i];
+        qx[i] = cs.x * x - cs.y * y;
+        qy[i] = bip_shift<W>(cs.y * x + cs.x * y, a);
+      }
+    }
+    __syncthreads();
+  }
+  const int yr = (a + ns) & (W - 1);
+  if constexpr (PHASE == 1) {
+    double* qo = T1 + (size_t)pair * N * N;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      qo[(size_t)(k0 + i) * N + a] = qx[i];
+      qo[(size_t)(k0 + i) * N + W + yr] = qy[i];
+    }
+  } else {
+    float* qo = Tq + (size_t)q * QN * QN;
+    const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      qo[(size_t)(k0 + i) * QN + xc] = (float)qx[i];
+      qo[(size_t)(k0 + i) * QN + yc] = (float)qy[i];
+    }
+  }
+}
+
+// Step-(s+1) couplings of quad q in Gram space, one workgroup per output
+// pair and column half (blockIdx.x = 2q + j, blockIdx.y = oj): j = 0
+// C(a',d') = L^T M R with L = Q_ac[:, :W] (rows a;c), M = [[C_ab, C_ad],
+// [C_cb, C_cd]] (rows a;c, columns b;d), R = Q_bd[:, W:]; j = 1 C(b',c') =
+// Q_bd[:, :W]^T M^T Q_ac[:, W:].  M is summed over the Gram's row chunks in
+// fp64, R's and L's columns are staged in LDS (fp32), both products on f32
+// MFMA (the data Gram is f32 MFMA as well).  Output: one W x W slab per pair
+// of step s+1 (nchunk = 1), the layout evd_cross_kernel reads.
+constexpr int kUpdThreads = 256;
+__global__ __launch_bounds__(kUpdThreads) void quad_update_kernel(
+    const float* __restrict__ slabs, int gch, const double* __restrict__ T1,
+    float* __restrict__ upd) {
+  constexpr int W = 64, N = 2 * W, MP = N + 4, HP = 32 + 4;
+  using M = Mfma<float>;
+  __shared__ float Ms[N * MP];
+  __shared__ float Rs[N * HP];  // R[:, 32 oj .. + 32]
+  __shared__ float Ys[N * HP];  // Y = Mx R_oj
+  __shared__ float Ls[N * (W + 4)];
+  const int q = blockIdx.x >> 1, j = blockIdx.x & 1, oj = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double* Rg = T1 + (size_t)(j == 0 ? 2 * q + 1 : 2 * q) * N * N + W + 32 * oj;
+  const double* Lg = T1 + (size_t)(j == 0 ? 2 * q : 2 * q + 1) * N * N;
+  for (int idx = tid; idx < N * 32; idx += kUpdThreads) {
+    const int r = idx >> 5, cc = idx & 31;
+    Rs[r * HP + cc] = (float)Rg[(size_t)r * N + cc];
+  }
+  for (int idx = tid; idx < N * W; idx += kUpdThreads) {
+    const int r = idx >> 6, cc = idx & 63;
+    Ls[r * (W + 4) + cc] = (float)Lg[(size_t)r * N + cc];
+  }
+  // slabs of quad q: r = 0 (a,d), 1 (b,c), 2 (a,b), 3 (c,d), gch chunks each
+  const float* base = slabs + (size_t)q * 4 * gch * W * W;
+  for (int idx = tid; idx < 4 * W * W; idx += kUpdThreads) {
+    const int r = idx / (W * W), e = idx % (W * W), i = e / W, jj = e % W;
+    const float* p = base + (size_t)r * gch * W * W + e;
+    double s = 0.0;
+    for (int k = 0; k < gch; ++k) s += (double)p[(size_t)k * W * W];
+    const int row = r == 0 ? i : r == 1 ? W + jj : r == 2 ? i : W + i;
+    const int col = r == 0 ? W + jj : r == 1 ? i : r == 2 ? jj : W + jj;
+    Ms[row * MP + col] = (float)s;
+  }
+  __syncthreads();
+  const int li = lane & 31, lk = lane >> 5;
+  {  // Y = Mx R_oj (N x 32): wave w owns row tile w
+    M::acc_t acc = M::zero();
+    const int i = wave * 32 + li;
+#pragma unroll 8
+    for (int l0 = 0; l0 < N; l0 += 2) {
+      const int l = l0 + lk;
+      const float av = j == 0 ? Ms[i * MP + l] : Ms[l * MP + i];
+      acc = M::mfma(av, Rs[l * HP + li], acc);
+    }
+#pragma unroll
+    for (int e = 0; e < M::NACC; ++e) Ys[(wave * 32 + M::acc_row(e, lane)) * HP + li] = acc[e];
+  }
+  __syncthreads();
+  if (wave < 2) {  // out[:, 32 oj ..] = Lx^T Y (W x 32): wave w owns row tile w
+    M::acc_t acc = M::zero();
+#pragma unroll 8
+    for (int k0 = 0; k0 < N; k0 += 2) {
+      const int k = k0 + lk;
+      acc = M::mfma(Ls[k * (W + 4) + wave * 32 + li], Ys[k * HP + li], acc);
+    }
+    float* out = upd + (size_t)blockIdx.x * W * W;
+#pragma unroll
+    for (int e = 0; e < M::NACC; ++e)
+      out[(wave * 32 + M::acc_row(e, lane)) * W + 32 * oj + li] = acc[e];
+  }
+}
+
+// T - I of every quad split into NP bf16 parts (split_bf16), in the A-operand
+// order of v_mfma_f32_32x32x16_bf16: entry [q][kb][ct][part][lane (c, h)]
+// element e = (T - I)[kb 16 + 8h + e][ct 32 + c].  One thread per
+// fragment; skipped quads are left alone (the apply skips them too).
+constexpr int kTsplitThreads = 256;
+template <int NP>
+__global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
+    const float* __restrict__ Tq, bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
+    const int32_t* __restrict__ skip2) {
+  constexpr int QN = 256;
+  const int q = blockIdx.x;
+  if (skip1[2 * q] && skip1[2 * q + 1] && skip2[2 * q] && skip2[2 * q + 1]) return;
+  const int idx = blockIdx.y * kTsplitThreads + threadIdx.x;  // < 16 * 8 * 64
+  const int kb = idx >> 9, ct = (idx >> 6) & 7, lane = idx & 63;
+  const int col = ct * 32 + (lane & 31), k0 = kb * 16 + 8 * (lane >> 5);
+  const float* src = Tq + (size_t)q * QN * QN + col;
+  bf16x8 parts[NP];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    __bf16 p[NP];
+    split_bf16<NP>(src[(size_t)k * QN] - (k == col ? 1.0f : 0.0f), p);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
+  }
+  bf16x8* dst = Ts + ((((size_t)q * 16 + kb) * 8 + ct) * NP) * SVDJ_WAVE + lane;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) dst[i * SVDJ_WAVE] = parts[i];
+}
+
+// [a b c d] <- [a b c d] T for 128 rows of A or V per workgroup, in place,
+// T the quad's 256 x 256 transform, split-bf16 delta form Y = X + X (T - I)
+// as apply_split_kernel (transposed: lane = row, coalesced loads/stores).
+// The workgroup owns ALL 256 output columns of its rows, so reading the
+// inputs and writing the outputs in place cannot race with another
+// workgroup (a two-workgroup split of the columns did: each reads all four
+// blocks).  T does not fit a CU's registers in split form (384 KB), so it is
+// streamed through LDS in K chunks of 32 columns (pre-split by
+// tsplit_kernel), double-buffered with the matching X chunk:
+//   8 waves, wave w owns rows 32 (w >> 1) .. + 32 and output column tiles
+//   4 (w & 1) .. + 3 (128 columns, 4 accumulators);
+//   per chunk: 2 k blocks x 4 tiles x 6 MFMAs per wave, operands by
+//   ds_read_b128 (X split image: [row group][k block][part][lane]);
+//   chunk kc is loaded by the four waves that output column tile kc, which
+//   keep its raw values (moved to accumulator lanes by v_permlane32_swap)
+//   for the epilogue.
+// Quad q's workgroups are placed on XCD group q % 8 (blockIdx % 8), so a
+// group's L2 holds the T of only nq / 8 quads.
+constexpr int kQuadApplyThreads = 512;
+constexpr int kQuadRows = 128;
+template <int NP>
+__global__ __launch_bounds__(kQuadApplyThreads) void apply_quad_kernel(
+    float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
+    const int32_t* __restrict__ pairs, int nq, const bf16x8* __restrict__ Ts,
+    const int32_t* __restrict__ skip1, const int32_t* __restrict__ skip2, int tpq) {
+  constexpr int W = 64, NKC = 8;
+  constexpr int TCH = 2 * 8 * NP * SVDJ_WAVE;  // T fragments per chunk
+  constexpr int TPT = TCH / kQuadApplyThreads;  // per thread
+  __shared__ bf16x8 Tl[2][TCH];
+  __shared__ bf16x8 Xl[2][4][2][NP][SVDJ_WAVE];
+
+  const int L = blockIdx.x;
+  int q, t;
+  if (nq % 8 == 0) {
+    const int g = nq / 8, s = L >> 3;
+    q = (s % g) * 8 + (L & 7);
+    t = s / g;
+  } else {
+    q = L % nq;
+    t = L / nq;
+  }
+  if (t >= tpq) return;
+  if (skip1[2 * q] && skip1[2 * q + 1] && skip2[2 * q] && skip2[2 * q + 1]) return;
+  float* base;
+  int ld, r0;
+  if (t < a_tiles) {
+    base = A;
+    ld = lda;
+    r0 = t * kQuadRows;
+  } else {
+    base = V;
+    ld = ldv;
+    r0 = (t - a_tiles) * kQuadRows;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int rg = wave >> 1, chh = wave & 1;
+  const int32_t* qp = pairs + 4 * q;  // (a, c), (b, d)
+  // column tile kc (32 columns) of the quad: block kc >> 1 in [a b c d] order
+  auto col_ptr = [&](int kc) -> float* {
+    const int qb = kc >> 1;
+    return base + (size_t)(qp[(qb & 1) * 2 + (qb >> 1)] * W + (kc & 1) * 32) * ld;
+  };
+  const bf16x8* Tq = Ts + (size_t)q * 16 * 8 * NP * SVDJ_WAVE;
+  const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
+  const uint32_t st_off = (uint32_t)(4 * h * ld + c);
+  const int rw = r0 + 32 * rg;  // this wave's rows
+
+  float xg[2][8];
+  bf16x8 tg[TPT];
+  float xo[4][16];
+  auto gload = [&](int kc) {
+    if ((kc >> 2) == chh) {  // the four loader waves of this chunk
+      const float* p = col_ptr(kc);
+#pragma unroll
+      for (int kbl = 0; kbl < 2; ++kbl)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          xg[kbl][e] = p[(size_t)(16 * kbl + e) * ld + (lane_off + (uint32_t)rw)];
+    }
+    const bf16x8* tp = Tq + (size_t)kc * TCH;
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) tg[j] = tp[j * kQuadApplyThreads + tid];
+  };
+  auto lstore = [&](int kc, int slot, int buf) {
+    if ((kc >> 2) == chh) {
+#pragma unroll
+      for (int kbl = 0; kbl < 2; ++kbl) {
+        bf16x8 parts[NP];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 p[NP];
+          split_bf16<NP>(xg[kbl][e], p);
+#pragma unroll
+          for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) Xl[buf][rg][kbl][i][lane] = parts[i];
+      }
+      // raw values of output tile kc in accumulator layout: register g*4+i
+      // of lane (c, h) is column 8g + 4h + i; lane half h loaded columns
+      // 16 kbl + 8h + e
+      float* xd = xo[slot];
+#pragma unroll
+      for (int kbl = 0; kbl < 2; ++kbl)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float keep = h ? xg[kbl][4 + i] : xg[kbl][i];
+          const float give = h ? xg[kbl][i] : xg[kbl][4 + i];
+          const float got = __int_as_float(half_swap(__float_as_int(give)));
+          xd[(2 * kbl) * 4 + i] = h ? got : keep;
+          xd[(2 * kbl + 1) * 4 + i] = h ? keep : got;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) Tl[buf][j * kQuadApplyThreads + tid] = tg[j];
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = Mfma<float>::zero();
+  gload(0);
+  lstore(0, 0, 0);
+  __syncthreads();
+  // chunk kc = 4 kq + ki: ki unrolled so the raw-value slots xo[ki] are
+  // static registers, kq rolled (a fully unrolled loop spilled)
+#pragma unroll 1
+  for (int kq = 0; kq < 2; ++kq) {
+#pragma unroll
+    for (int ki = 0; ki < 4; ++ki) {
+      const int kc = 4 * kq + ki, buf = ki & 1;
+      if (kc + 1 < NKC) gload(kc + 1);
+#pragma unroll
+      for (int kbl = 0; kbl < 2; ++kbl) {
+        bf16x8 xs[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) xs[i] = Xl[buf][rg][kbl][i][lane];
+#pragma unroll
+        for (int ot = 0; ot < 4; ++ot) {
+          const int ct = 4 * chh + ot;
+          bf16x8 qf[NP];
+#pragma unroll
+          for (int i = 0; i < NP; ++i) qf[i] = Tl[buf][((kbl * 8 + ct) * NP + i) * SVDJ_WAVE + lane];
+          // small products first, the leading one last, one accumulator:
+          // a second one for the small terms (apply_split_kernel) does not fit
+          // next to the 4 x 16 raw values (spills); a quad applies T to each
+          // column half as often as two single steps
+          acc[ot] = mfma_split<NP, 1>(qf, xs, acc[ot]);
+          acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[0], xs[0], acc[ot], 0, 0, 0);
+        }
+      }
+      if (kc + 1 < NKC) lstore(kc + 1, (ki + 1) & 3, buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // every read of this workgroup's rows is done: store in place
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    float* p = col_ptr(4 * chh + ot);
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      p[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)rw)] = xo[ot][e] + acc[ot][e];
+  }
+}
+
 // ------------------------------------------------------------- host side
 struct Geometry {
   int gchunks, grows;  // gram
   int a_chunks, rows_a, v_chunks, rows_v;
+  // quad steps (fp32 W = 64): gram row chunks, apply row chunks
+  int qgch, qgrows, qa_chunks, qv_chunks, qrows;
 };
+
+// Quad-step geometry: the GRAM_QUAD launch has 3P workgroups per row chunk
+// and each of its slabs is summed by evd_cross_kernel / quad_update_kernel,
+// so it uses few chunks (~512 workgroups); the apply has 2 workgroups per
+// quad and row chunk, one per CU (LDS), ~4096 of them.
+static void quad_geometry(Geometry& g, int P, int m_pad, int n_v) {
+  const int want = (512 + 3 * P - 1) / (3 * P);
+  const int maxc = m_pad / 128;
+  g.qgch = want < 1 ? 1 : (want > maxc ? maxc : want);
+  g.qgrows = round_up((m_pad + g.qgch - 1) / g.qgch, 128);
+  g.qgch = (m_pad + g.qgrows - 1) / g.qgrows;
+  g.qrows = kQuadRows;
+  g.qa_chunks = (m_pad + kQuadRows - 1) / kQuadRows;
+  g.qv_chunks = n_v > 0 ? (n_v + kQuadRows - 1) / kQuadRows : 0;
+}
 
 static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   Geometry g;
@@ -1707,10 +2118,25 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   g.rows_v = rows;
   g.a_chunks = (m_pad + rows - 1) / rows;
   g.v_chunks = n_v > 0 ? (n_v + rows - 1) / rows : 0;
+  quad_geometry(g, P, m_pad, n_v);
   return g;
 }
 
 static size_t rup256(size_t b) { return (b + 255) / 256 * 256; }
+// Quad-step scratch (fp32 W = 64 only): GRAM_QUAD slabs (3P pairs), T1
+// (fp64 Q of the P step-s pairs), the step-(s+1) couplings, T (P/2 quads x
+// 256 x 256 fp32), and double-buffered split T (3 parts) and skip flags of
+// both EVDs.
+static bool has_quad(int esize, int W) { return esize == 4 && W == 64; }
+static size_t quad_bytes(int P, int m_pad) {
+  Geometry g;
+  quad_geometry(g, P, m_pad, 0);
+  constexpr int W = 64;
+  const size_t sk = rup256((size_t)P * sizeof(int32_t));
+  return rup256((size_t)3 * P * g.qgch * W * W * sizeof(float)) +
+         rup256((size_t)P * 4 * W * W * sizeof(double)) + rup256((size_t)P * W * W * sizeof(float)) +
+         3 * rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float)) * 2 + 4 * sk;
+}
 static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   Geometry g = make_geometry(W, P, m_pad, 0);
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
@@ -1720,7 +2146,8 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   // slabs + double-buffered Q and skip flags (evd(s+1) may run while apply(s)
   // reads) + the cross EVD's rotation records and step counts (consumed by
   // qbuild(s) before evd(s+1) on the same stream: single-buffered)
-  return rup256(slabs) + 2 * rup256(q) + 2 * rup256(sk) + rup256(rec) + rup256(sk);
+  return rup256(slabs) + 2 * rup256(q) + 2 * rup256(sk) + rup256(rec) + rup256(sk) +
+         (has_quad(esize, W) ? quad_bytes(P, m_pad) : 0);
 }
 
 // One chain of steps: resident buffers, its pair list and its workspace.
@@ -1736,6 +2163,14 @@ struct Chain {
   int32_t* skipb[2];
   Pair2<double>* rec;  // cross EVD rotation records
   int32_t* nsteps;
+  // quad steps (has_quad)
+  float* qslabs;
+  double* T1;
+  float* upd;
+  float* Tq;
+  bf16x8* Ts[2];
+  int32_t* skip1[2];
+  int32_t* skip2[2];
   hipStream_t st;
 };
 
@@ -1769,19 +2204,96 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   c.rec = (Pair2<double>*)w;
   w += rup256((size_t)P * kCrossMaxInner * W * W * sizeof(Pair2<double>));
   c.nsteps = (int32_t*)w;
+  w += kstride;
+  c.qslabs = nullptr;
+  c.T1 = nullptr;
+  c.upd = nullptr;
+  c.Tq = nullptr;
+  c.Ts[0] = c.Ts[1] = nullptr;
+  c.skip1[0] = c.skip1[1] = c.skip2[0] = c.skip2[1] = nullptr;
+  if (has_quad(sizeof(T), W)) {
+    c.qslabs = (float*)w;
+    w += rup256((size_t)3 * P * c.g.qgch * W * W * sizeof(float));
+    c.T1 = (double*)w;
+    w += rup256((size_t)P * 4 * W * W * sizeof(double));
+    c.upd = (float*)w;
+    w += rup256((size_t)P * W * W * sizeof(float));
+    const size_t tstride = rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float));
+    c.Tq = (float*)w;
+    w += tstride;
+    c.Ts[0] = (bf16x8*)w;  // 3 bf16 parts = 1.5 x the fp32 size
+    c.Ts[1] = (bf16x8*)(w + 3 * tstride / 2);
+    w += 3 * tstride;
+    c.skip1[0] = (int32_t*)w;
+    c.skip1[1] = (int32_t*)(w + kstride);
+    c.skip2[0] = (int32_t*)(w + 2 * kstride);
+    c.skip2[1] = (int32_t*)(w + 3 * kstride);
+  }
   return 0;
+}
+
+// Quad step s (steps s, s+1 fused; see "quad step"): gram, evd 1, T1,
+// update, evd 2, T on the chain's stream.
+template <typename T, int W>
+static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmode, int max_inner,
+                                uint32_t* metric, int mma) {
+  if constexpr (sizeof(T) == 4 && W == 64) {
+    if (c.P % 2 || s + 1 >= c.steps || c.modes[s + 1] != 5) {
+      set_error("quad step %d: needs an even pair count (%d) and a following mode-5 step", s, c.P);
+      return -2;
+    }
+    const int b = s & 1;
+    const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
+    const int32_t* pr1 = pr + 2 * c.P;
+    hipLaunchKernelGGL((gram_kernel<float, 64, GRAM_QUAD>), dim3(3 * c.P, c.g.qgch, 1),
+                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.qgrows, c.qslabs);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
+                       pr, c.qslabs, c.g.qgch, c.D, c.rec, c.nsteps, c.skip1[b], (float)tol,
+                       absmode, max_inner, metric);
+    SVDJ_LAUNCH_CHECK();
+    constexpr int R = 8;
+    hipLaunchKernelGGL((qbuild_quad_kernel<1, R>), dim3(c.P, 128 / (R * 4)), dim3(kQbThreads), 0,
+                       c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(quad_update_kernel, dim3(c.P, 2), dim3(kUpdThreads), 0, c.st,
+                       c.qslabs + (size_t)c.P * c.g.qgch * 64 * 64, c.g.qgch, c.T1, c.upd);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
+                       pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,
+                       max_inner, metric);
+    SVDJ_LAUNCH_CHECK();
+    hipLaunchKernelGGL((qbuild_quad_kernel<2, R>), dim3(c.P, 256 / (R * 4)), dim3(kQbThreads), 0,
+                       c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    SVDJ_LAUNCH_CHECK();
+    const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
+    if (mma == 2)
+      hipLaunchKernelGGL((tsplit_kernel<2>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
+                         c.skip1[b], c.skip2[b]);
+    else
+      hipLaunchKernelGGL((tsplit_kernel<3>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
+                         c.skip1[b], c.skip2[b]);
+    SVDJ_LAUNCH_CHECK();
+    return 0;
+  } else {
+    (void)c; (void)s; (void)tol; (void)absmode; (void)max_inner; (void)metric; (void)mma;
+    set_error("quad steps need fp32 data and W = 64");
+    return -3;
+  }
 }
 
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
 template <typename T, int W>
 static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, int max_inner,
-                           uint32_t* metric) {
+                           uint32_t* metric, int mma) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
   // 0 cross (cyclic EVD), 1 full Gram, 2 cross + bipartite EVD, 3 cross +
   // cross-only bipartite EVD (evd_cross_kernel)
   const int mode = c.modes ? c.modes[s] : 0;
+  if (mode == 5) return 0;  // second step of a quad: done by its first (mode 4)
+  if (mode == 4) return launch_quad_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric, mma);
   const int full = mode == 1;
   constexpr int XS = gram_xsplit<T, W>();
   if (full) {
@@ -1828,6 +2340,32 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
   const int nv = c.V ? c.n_v : 0, ych = c.V ? c.g.v_chunks : 0;
+  const int mode = c.modes ? c.modes[s] : 0;
+  if (mode == 5) return 0;
+  if (mode == 4) {
+    if constexpr (sizeof(T) == 4 && W == 64) {
+      if (mma != 1 && mma != 2) {
+        set_error("quad steps run the split-bf16 apply (mma 1 or 2), got %d", mma);
+        return -3;
+      }
+      const int nq = c.P / 2, qv = c.V ? c.g.qv_chunks : 0;
+      const int tpq = c.g.qa_chunks + qv;
+      const dim3 grid(nq * tpq);
+      if (mma == 1)
+        hipLaunchKernelGGL((apply_quad_kernel<3>), grid, dim3(kQuadApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.qa_chunks, c.V, c.ldv, pr, nq, c.Ts[b], c.skip1[b],
+                           c.skip2[b], tpq);
+      else
+        hipLaunchKernelGGL((apply_quad_kernel<2>), grid, dim3(kQuadApplyThreads), 0, c.st, c.A,
+                           c.lda, c.g.qa_chunks, c.V, c.ldv, pr, nq, c.Ts[b], c.skip1[b],
+                           c.skip2[b], tpq);
+      SVDJ_LAUNCH_CHECK();
+      return 0;
+    } else {
+      set_error("quad steps need fp32 data and W = 64");
+      return -3;
+    }
+  }
   const dim3 grid(c.P, c.g.a_chunks + ych);
   if constexpr (sizeof(T) == 4) {
     if (mma == 1 || mma == 2) {
@@ -1864,7 +2402,7 @@ template <typename T, int W>
 static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inner,
                          uint32_t* metric, int mma) {
   for (int s = 0; s < c.steps; ++s) {
-    int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric);
+    int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric, mma);
     if (!rc) rc = launch_apply<T, W>(c, s, mma);
     if (rc) return rc;
   }
@@ -1928,13 +2466,13 @@ static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int 
   for (int s = 0; s < n; ++s) {
     int rc = 0;
     if (s < a.steps) {
-      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric);
+      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric, mma);
       if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
       if (!rc) rc = launch_apply<T, W>(a, s, mma);
     }
     if (!rc && s < b.steps) {
       if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric);
+      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric, mma);
       if (!rc) rc = launch_apply<T, W>(b, s, mma);
     }
     if (rc) {

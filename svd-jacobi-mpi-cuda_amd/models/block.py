@@ -78,6 +78,32 @@ def choose_mma(dtype: torch.dtype, W: int) -> str:
     return "bf16x6" if (dtype == torch.float32 and W == 64) else "native"
 
 
+def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
+    """Quad steps exist for fp32 W=64 with the split-bf16 apply and k
+    (blocks per super-block) a multiple of 4."""
+    return dtype == torch.float32 and W == 64 and mma in ("bf16x6", "bf16x3") and k % 4 == 0
+
+
+def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
+    """Quad steps for config quad="auto": off.  Measured on MI355X, 16384^2
+    fp32 1 GPU (profiles/r4_quad): the fused K = 256 apply reads T (384 KB
+    split per quad) from L2/MALL for every 128-row tile and ran at 1.71 ms
+    per quad step vs 2 x 0.70 ms for the two W = 64 applies it replaces;
+    whole solve 5.38 s vs 4.87 s.  Selectable with quad="on"."""
+    return False
+
+
+def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
+    if mode == "off":
+        return False
+    if mode == "on":
+        if not quad_supported(dtype, W, mma, k):
+            raise ValueError(f"quad steps need fp32, W=64, a split-bf16 apply and k % 4 == 0 "
+                             f"(dtype={dtype}, W={W}, mma={mma}, k={k})")
+        return True
+    return choose_quad(dtype, W, mma, k, P)
+
+
 def resolve_inner_order(order: str, W: int, pairs_per_step: int,
                         dtype: torch.dtype = torch.float32) -> str:
     return choose_inner_order(W, pairs_per_step, dtype) if order == "auto" else order

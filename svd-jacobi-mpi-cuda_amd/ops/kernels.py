@@ -281,6 +281,15 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             _stream(At)), "block_steps")
     else:
         for s in range(steps):
+            if modes[s] == 5:  # second step of a quad: done with its first
+                continue
+            if modes[s] == 4:
+                mx, nrot = ref.quad_step(At[:, :m_pad], Vt, D, pairs[s], pairs[s + 1], W, tol,
+                                         max_inner, tol_mode=tol_mode_code(tol_mode),
+                                         floor=float(metric[2]) if metric.numel() > 2 else 0.0)
+                metric[0] = max(float(metric[0]), mx)
+                metric[1] += nrot
+                continue
             mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
                                       max_inner, tol_mode=tol_mode_code(tol_mode),
                                       floor=float(metric[2]) if metric.numel() > 2 else 0.0,

@@ -199,6 +199,74 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
     return maxconv, int(rotated.sum())
 
 
+def quad_step(At, Vt, D, pairs0, pairs1, W, tol, max_inner, tol_mode: int = 0,
+              floor: float = 0.0):
+    """Two cross steps fused as one quad step (csrc/hip/block.hip "quad
+    step"), on the quads of ``pairs0`` ((a,c), (b,d) per quad) and
+    ``pairs1`` ((a,d), (b,c)).  The couplings of the second step come from
+    the Gram blocks of the first and its rotations (Gram space), the two
+    EVDs are cross-only, and the data is updated once by T = T1 T2.
+    Returns (maxconv, pairs_rotated) over both steps."""
+    Q = pairs0.shape[0] // 2
+    if Q == 0:
+        return 0.0, 0
+    p0, p1 = pairs0.long().view(Q, 2, 2), pairs1.long().view(Q, 2, 2)
+    a, c, b, d = p0[:, 0, 0], p0[:, 0, 1], p0[:, 1, 0], p0[:, 1, 1]
+    if not (bool((p1[:, 0, 0] == a).all()) and bool((p1[:, 0, 1] == d).all())
+            and bool((p1[:, 1, 0] == b).all()) and bool((p1[:, 1, 1] == c).all())):
+        raise ValueError("quad steps need pairs (a,c),(b,d) then (a,d),(b,c)")
+    ar = torch.arange(W)
+    blk = torch.stack([a, b, c, d], 1)                       # (Q, 4) in [a b c d] order
+    cols = (blk[:, :, None] * W + ar).reshape(Q, 4 * W)      # quad columns
+    X = At[cols]                                             # (Q, 4W, ld)
+    G = X @ X.transpose(1, 2)                                # only off-diagonal blocks used
+    Dq = D[cols]
+    N = 2 * W
+    ia, ib, ic, id_ = (torch.arange(W) + k * W for k in range(4))
+
+    def evd(x_idx, y_idx, C):
+        Gp = torch.zeros(C.shape[0], N, N, dtype=At.dtype)
+        n_idx = torch.arange(N)
+        Gp[:, n_idx, n_idx] = torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1)
+        Gp[:, :W, W:] = C
+        Gp[:, W:, :W] = C.transpose(1, 2)
+        dg = torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1).clamp(min=0).sqrt()
+        den = dg[:, :W, None] * dg[:, None, W:]
+        R = torch.where(den > 0, C.abs() / torch.where(den > 0, den, torch.ones_like(den)),
+                        torch.zeros_like(den))
+        if tol_mode != 1 and floor > 0:
+            big = torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1) > floor
+            R = torch.where(big[:, :W, None] & big[:, None, W:], R, torch.zeros_like(R))
+        mx = float(R.max()) if R.numel() else 0.0
+        lam, Qm, rot = jacobi_evd(Gp, tol, max_inner, tol_mode, order="cross", floor=floor)
+        lam = torch.where(rot[:, None], lam, torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1))
+        Dq[:, x_idx], Dq[:, y_idx] = lam[:, :W], lam[:, W:]
+        eye = torch.eye(N, dtype=At.dtype).expand_as(Qm)
+        return torch.where(rot[:, None, None], Qm, eye), mx, int(rot.sum())
+
+    Qac, m1, r1 = evd(ia, ic, G[:, ia][:, :, ic])
+    Qbd, m2, r2 = evd(ib, id_, G[:, ib][:, :, id_])
+    T1 = torch.zeros(Q, 4 * W, 4 * W, dtype=At.dtype)
+    ac, bd = torch.cat([ia, ic]), torch.cat([ib, id_])
+    T1[:, ac[:, None], ac[None, :]] = Qac
+    T1[:, bd[:, None], bd[None, :]] = Qbd
+    G1 = T1.transpose(1, 2) @ G @ T1                         # Gram of [a' b' c' d']
+    Qad, m3, r3 = evd(ia, id_, G1[:, ia][:, :, id_])
+    Qbc, m4, r4 = evd(ib, ic, G1[:, ib][:, :, ic])
+    T2 = torch.zeros_like(T1)
+    ad, bc = torch.cat([ia, id_]), torch.cat([ib, ic])
+    T2[:, ad[:, None], ad[None, :]] = Qad
+    T2[:, bc[:, None], bc[None, :]] = Qbc
+    T = T1 @ T2
+    nrot = r1 + r2 + r3 + r4
+    if nrot:
+        At[cols] = T.transpose(1, 2) @ X
+        if Vt is not None:
+            Vt[cols] = T.transpose(1, 2) @ Vt[cols]
+    D[cols] = Dq
+    return max(m1, m2, m3, m4), nrot
+
+
 def col_norms2(At):
     return (At.double() ** 2).sum(1).to(At.dtype)
 

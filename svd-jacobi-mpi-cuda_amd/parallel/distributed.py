@@ -35,7 +35,7 @@ import torch
 from ..config import SolverConfig, SVDOptions
 from ..models.base import SVDResult, Solver
 from ..models import precondition as pre
-from ..models.block import choose_block, choose_mma, resolve_inner_order
+from ..models.block import choose_block, choose_mma, resolve_inner_order, resolve_quad
 from ..ops import kernels as K
 from ..utils import checkpoint as ckpt
 from ..utils.layout import pad_rows, round_up
@@ -232,8 +232,9 @@ class DistributedBlockJacobi(Solver):
         g = comm.rank
         tour = tournament(P)
         pipelined = cfg.chains == 2
+        quad = pipelined and resolve_quad(cfg.quad, dtype, W, mma, k, P)
         if pipelined:
-            splan = sweep_plan(P, k, tour.xslot[:, g])
+            splan = sweep_plan(P, k, tour.xslot[:, g], quad=quad)
         else:
             plans = distributed_sweep_plan(P, k)
             dev_pairs = [torch.from_numpy(p.pairs).to(dev) for p in plans]
@@ -352,7 +353,7 @@ class DistributedBlockJacobi(Solver):
         sync()
         t_total = time.perf_counter() - t0
         info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
-                "inner_order": inner,
+                "inner_order": inner, "quad": quad,
                 "exchange": ex.exchange if pipelined else "direct",
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
         if pipelined and P > 1:

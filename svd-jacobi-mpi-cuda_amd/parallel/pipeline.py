@@ -35,7 +35,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .schedule import round_robin
+from .schedule import (quad_bipartite, quad_bipartite_modes, quad_round_robin,
+                       quad_round_robin_modes, round_robin)
 from .spread import relay_chunk, resolve_exchange, spread_ops
 
 
@@ -79,18 +80,25 @@ def _bipartite(xs: list, ys: list) -> np.ndarray:
     return out
 
 
-def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2) -> SweepPlan:
+def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2, quad: bool = False
+               ) -> SweepPlan:
     """Items of one sweep.  ``xslot[r]`` is the slot replaced before round r
     (r >= 1), as produced by schedule.tournament.  (Four chains in quarters
     were measured slower than two at every P in round 2 -- 8-GPU plan 64 ->
-    84-88 ms per sweep -- and removed.)"""
+    84-88 ms per sweep -- and removed.)  ``quad``: the same block pairs in
+    quad order (schedule.quad_round_robin / quad_bipartite, mode 4/5 steps
+    fused two at a time, csrc/hip/block.hip "quad step"); needs k % 4 == 0."""
     if chains != 2:
         raise ValueError(f"pipelined sweep: 2 chains, got {chains}")
     if k < 2 or k % 2:
         raise ValueError(f"pipelined sweep needs an even block count per super-block, got {k}")
+    if quad and k % 4:
+        raise ValueError(f"quad steps need a multiple of 4 blocks per super-block, got {k}")
     plan = SweepPlan(P, k)
-    rr = round_robin(k)
-    rr_modes = [1] + [0] * (k - 2)
+    if quad:
+        rr, rr_modes = quad_round_robin(k), quad_round_robin_modes(k)
+    else:
+        rr, rr_modes = round_robin(k), [1] + [0] * (k - 2)
     plan.items.append(Task("rr0", rr.copy(), rr_modes, 0, ((0, 0), (0, 1))))
     plan.items.append(Task("rr1", rr + k, rr_modes, 1, ((1, 0), (1, 1))))
     R = 2 * P - 1
@@ -100,8 +108,11 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2) -> SweepPlan:
         h = k // 2
 
         def task(name, ih, sh, stream):
-            return Task(f"r{r}.{name}", _bipartite(_blocks(inc, ih, k), _blocks(stay, sh, k)),
-                        [0] * h, stream, ((inc, ih), (stay, sh)))
+            xs, ys = _blocks(inc, ih, k), _blocks(stay, sh, k)
+            if quad:
+                return Task(f"r{r}.{name}", quad_bipartite(xs, ys), quad_bipartite_modes(h), stream,
+                            ((inc, ih), (stay, sh)))
+            return Task(f"r{r}.{name}", _bipartite(xs, ys), [0] * h, stream, ((inc, ih), (stay, sh)))
 
         nxt = int(xslot[r + 1]) if r + 1 < R else None
         if nxt is None:

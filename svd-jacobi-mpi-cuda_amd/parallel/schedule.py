@@ -84,6 +84,86 @@ def tournament(P: int) -> Tournament:
     return Tournament(P, held, xs, st, rf)
 
 
+# ------------------------------------------------------- quad-step orders
+# A quad step (csrc/hip/block.hip "quad step") fuses two cross steps over
+# the four blocks (a, b, c, d): step s pairs (a, c), (b, d), step s+1 pairs
+# (a, d), (b, c), i.e. all cross pairs of the super-block pair {a, b} x
+# {c, d}.  Pair 2q / 2q+1 of both steps belong to quad q, in that
+# orientation (the kernels read the quad from the pair lists).  Mode codes:
+# 4 = first step of a quad (does both), 5 = its second step.
+QUAD_HEAD, QUAD_TAIL = 4, 5
+
+
+def quad_round_robin(nb: int) -> np.ndarray:
+    """(nb-1, nb//2, 2) block pairs covering every pair of nb blocks once,
+    nb % 4 == 0: step 0 pairs the two blocks of every super-block (2i, 2i+1)
+    (the full-Gram step of a sweep), then a round robin over the nb/2
+    super-blocks, each super-step as the two steps of a quad."""
+    if nb < 4 or nb % 4:
+        raise ValueError(f"quad_round_robin needs a multiple of 4 blocks, got {nb}")
+    K = nb // 2
+    out = _i32((nb - 1, K, 2))
+    out[0, :, 0] = np.arange(0, nb, 2)
+    out[0, :, 1] = np.arange(1, nb, 2)
+    srr = round_robin(K)
+    for t in range(K - 1):
+        for q, (I, J) in enumerate(srr[t]):
+            a, b, c, d = 2 * I, 2 * I + 1, 2 * J, 2 * J + 1
+            out[1 + 2 * t, 2 * q] = (a, c)
+            out[1 + 2 * t, 2 * q + 1] = (b, d)
+            out[2 + 2 * t, 2 * q] = (a, d)
+            out[2 + 2 * t, 2 * q + 1] = (b, c)
+    return out
+
+
+def quad_round_robin_modes(nb: int) -> list:
+    return [1] + [QUAD_HEAD, QUAD_TAIL] * (nb // 2 - 1)
+
+
+def quad_bipartite(xs, ys) -> np.ndarray:
+    """(h, h, 2) cross pairs between block lists xs and ys (h = len, even)
+    in quad order: super-step t pairs super-block (xs[2i], xs[2i+1]) with
+    (ys[2j], ys[2j+1]), j = (i + t) mod h/2."""
+    h = len(xs)
+    if h < 2 or h % 2 or len(ys) != h:
+        raise ValueError(f"quad_bipartite needs two even lists of equal length, got {h}, {len(ys)}")
+    H = h // 2
+    out = _i32((h, h, 2))
+    for t in range(H):
+        for i in range(H):
+            j = (i + t) % H
+            a, b, c, d = xs[2 * i], xs[2 * i + 1], ys[2 * j], ys[2 * j + 1]
+            out[2 * t, 2 * i] = (a, c)
+            out[2 * t, 2 * i + 1] = (b, d)
+            out[2 * t + 1, 2 * i] = (a, d)
+            out[2 * t + 1, 2 * i + 1] = (b, c)
+    return out
+
+
+def quad_bipartite_modes(h: int) -> list:
+    return [QUAD_HEAD, QUAD_TAIL] * (h // 2)
+
+
+def check_quad_steps(pairs: np.ndarray, modes) -> None:
+    """Raise ValueError unless every mode-4 step and the following mode-5
+    step hold quads in the orientation the kernels read."""
+    modes = [int(x) for x in modes]
+    for s, md in enumerate(modes):
+        if md == QUAD_TAIL and (s == 0 or modes[s - 1] != QUAD_HEAD):
+            raise ValueError(f"step {s}: quad tail without head")
+        if md != QUAD_HEAD:
+            continue
+        if s + 1 >= len(modes) or modes[s + 1] != QUAD_TAIL:
+            raise ValueError(f"step {s}: quad head without tail")
+        p0, p1 = pairs[s], pairs[s + 1]
+        if p0.shape[0] % 2:
+            raise ValueError(f"step {s}: odd pair count {p0.shape[0]}")
+        for q in range(p0.shape[0] // 2):
+            (a, c), (b, d) = p0[2 * q], p0[2 * q + 1]
+            if tuple(p1[2 * q]) != (a, d) or tuple(p1[2 * q + 1]) != (b, c):
+                raise ValueError(f"steps {s},{s + 1} quad {q}: not (a,c),(b,d) / (a,d),(b,c)")
+
+
 # ------------------------------------------------------------ python twins
 def sameh_py(n: int) -> np.ndarray:
     M = (n + 1) // 2

@@ -3,6 +3,7 @@ apply_split_kernel): the 3-way round-to-nearest bf16 split is accurate to
 2^-27, and the six order < 3 products of X (Q - I), added to X in fp32,
 reproduce X Q to fp32 rounding.  The GPU kernel itself is checked against the
 f32 MFMA apply in tests/test_gpu_kernels.py (test_bf16x6_matches_native)."""
+import pytest
 import torch
 
 
@@ -42,3 +43,30 @@ def test_delta_form_matches_fp32_product():
         ref = X.double() @ Q.double()
         err = (Y.double() - ref).abs().max() / ref.abs().max()
         assert float(err) < 4 * 2.0 ** -24, float(err)
+
+
+@pytest.mark.parametrize("inner", [1, 3])
+def test_reference_quad_step_equals_two_cross_steps(inner):
+    """ops.reference.quad_step (Gram-space couplings for the second step, T =
+    T1 T2 applied once) equals the two cross steps it fuses, in fp64."""
+    import torch
+    import svdj
+    R, S = svdj.ops.reference, svdj.parallel.schedule
+    torch.manual_seed(0)
+    W, nb, m = 16, 8, 300
+    n = nb * W
+    A = torch.rand(n, m, dtype=torch.float64)
+    for b in range(nb):
+        q, _ = torch.linalg.qr(A[b * W:(b + 1) * W].t())
+        A[b * W:(b + 1) * W] = (q * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+    pr = torch.from_numpy(S.quad_round_robin(nb))
+    At1, Vt1 = A.clone(), torch.eye(n, dtype=torch.float64)
+    D1 = R.col_norms2(At1)
+    At2, Vt2, D2 = At1.clone(), Vt1.clone(), D1.clone()
+    m1a, r1a = R.block_step(At1, Vt1, D1, pr[1], W, False, 1e-12, inner, order="cross")
+    m1b, r1b = R.block_step(At1, Vt1, D1, pr[2], W, False, 1e-12, inner, order="cross")
+    m2, r2 = R.quad_step(At2, Vt2, D2, pr[1], pr[2], W, 1e-12, inner)
+    assert r2 == r1a + r1b == nb
+    assert abs(m2 - max(m1a, m1b)) < 1e-12
+    for x, y in ((At1, At2), (Vt1, Vt2), (D1, D2)):
+        assert float((x - y).abs().max()) < 1e-13

@@ -234,3 +234,22 @@ def test_native_mma_rule_matches_python():
     assert cfg.resolved_mma(A, 64) == "bf16x6" and cfg.resolved_mma(A, 32) == "native"
     assert cfg.resolved_mma(A.double(), 64) == "native"
     assert svdj.SolverConfig(mma="native").resolved_mma(A, 64) == "native"
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("k", [4, 8, 12])
+def test_quad_plan_meets_every_pair_once(P, k):
+    """Quad order (two cross steps fused per quad): the same coverage, and
+    every mode-4/5 step pair holds quads in the kernels' orientation."""
+    tour = schedule.tournament(P)
+    plans = [pipeline.sweep_plan(P, k, tour.xslot[:, g], quad=True) for g in range(P)]
+    pipeline.check_plan_coverage(plans, tour)
+    for it in plans[0].items:
+        if isinstance(it, pipeline.Task):
+            schedule.check_quad_steps(it.pairs, it.modes)
+            assert 4 in it.modes
+
+
+def test_quad_plan_needs_multiple_of_4():
+    with pytest.raises(ValueError):
+        pipeline.sweep_plan(1, 6, schedule.tournament(1).xslot[:, 0], quad=True)

@@ -499,3 +499,35 @@ def test_evd_deal_table_valid_and_cheaper(W):
     c_opt, _ = T.deal_cost(W, T.BIP, slots)
     c_r2, _ = T.deal_cost(W, T.BIP, T.slots_from(duty, rest, W))
     assert c_opt < 0.8 * c_r2, (c_opt, c_r2)
+
+
+@pytest.mark.parametrize("nb", [4, 8, 16, 64])
+def test_quad_round_robin_covers_once(nb):
+    pr = S.quad_round_robin(nb)
+    modes = S.quad_round_robin_modes(nb)
+    assert pr.shape == (nb - 1, nb // 2, 2) and len(modes) == nb - 1
+    S.check_quad_steps(pr, modes)
+    seen = set()
+    for st in pr:
+        assert sorted(st.ravel().tolist()) == list(range(nb))
+        seen |= {(min(a, b), max(a, b)) for a, b in st.tolist()}
+    assert len(seen) == nb * (nb - 1) // 2
+    assert pr[0].tolist() == [[2 * i, 2 * i + 1] for i in range(nb // 2)]
+
+
+@pytest.mark.parametrize("h", [2, 4, 8])
+def test_quad_bipartite_covers_once(h):
+    xs, ys = list(range(h)), list(range(100, 100 + h))
+    pr = S.quad_bipartite(xs, ys)
+    S.check_quad_steps(pr, S.quad_bipartite_modes(h))
+    assert {(a, b) for st in pr for a, b in st.tolist()} == {(x, y) for x in xs for y in ys}
+
+
+def test_check_quad_steps_rejects_wrong_orientation():
+    pr = S.quad_round_robin(8)
+    bad = pr.copy()
+    bad[2, 0] = bad[2, 0, ::-1]
+    with pytest.raises(ValueError):
+        S.check_quad_steps(bad, S.quad_round_robin_modes(8))
+    with pytest.raises(ValueError):
+        S.check_quad_steps(pr, [1, 5, 4] + [4, 5] * 2)
