@@ -449,8 +449,10 @@ def run_native(a, dtype, work):
                        "staggered": bool(a.stagger), "root_owned": False},
             "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
-            "comm": ({"comm_ms": round(p.comm_ms, 3), "exposed_comm_ms": round(p.exposed_comm_ms, 3)}
-                     if a.comm_timing else None),
+            "comm": ({"exchanges": int(p.exchanges), "bytes_sent": int(p.bytes_sent),
+                      "timing": bool(a.comm_timing),
+                      **({"comm_ms": round(p.comm_ms, 3), "exposed_comm_ms": round(p.exposed_comm_ms, 3)}
+                         if a.comm_timing else {})} if world > 1 else None),
             "world": world, "rccl_ranks": world,
             "accuracy": acc,
         }

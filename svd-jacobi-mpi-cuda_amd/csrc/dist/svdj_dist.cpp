@@ -31,6 +31,8 @@
 #include <mutex>
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <tuple>
@@ -96,39 +98,68 @@ struct Task {
 
 extern "C" const char* svdj_dist_last_error(void) { return g_err; }
 
+// The id file carries a job token next to the RCCL id, so a rank accepts
+// only the file of its own job: SVDJ_JOB_TOKEN (svdj_dist_main --np sets a
+// fresh one before forking) or torchrun's TORCHELASTIC_RUN_ID.  Without a
+// token, a file written within timeout_s before this call is accepted (a
+// crashed job's file younger than that would be taken: launchers without a
+// token remove the file before their own rendezvous, as bench.py does).
+namespace {
+struct IdFile {
+  char magic[8];
+  char token[64];
+  ncclUniqueId id;
+};
+constexpr char kIdMagic[8] = {'S', 'V', 'D', 'J', 'I', 'D', '2', 0};
+std::string job_token() {
+  const char* t = std::getenv("SVDJ_JOB_TOKEN");
+  if (t && *t) return std::string(t).substr(0, 63);
+  const char* r = std::getenv("TORCHELASTIC_RUN_ID");
+  if (r && *r && std::strcmp(r, "none")) return std::string(r).substr(0, 63);
+  return std::string();
+}
+}  // namespace
+
 extern "C" int svdj_dist_comm_init(int rank, int world, const char* id_path, double timeout_s,
                                    void** comm) {
-  ncclUniqueId id;
-  const std::string path(id_path);
+  IdFile rec;
+  std::memset(&rec, 0, sizeof(rec));
+  const std::string path(id_path), token = job_token();
   if (rank == 0) {
-    NCCLC(ncclGetUniqueId(&id));
+    NCCLC(ncclGetUniqueId(&rec.id));
+    std::memcpy(rec.magic, kIdMagic, sizeof(kIdMagic));
+    std::memcpy(rec.token, token.data(), token.size());
     const std::string tmp = path + ".tmp";
     FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f || fwrite(&id, sizeof(id), 1, f) != 1) return fail(-1, "cannot write %s", tmp.c_str());
+    if (!f || fwrite(&rec, sizeof(rec), 1, f) != 1) return fail(-1, "cannot write %s", tmp.c_str());
     fclose(f);
     if (rename(tmp.c_str(), path.c_str()) != 0) return fail(-1, "cannot publish %s", path.c_str());
   } else {
-    // A file left by a crashed earlier job on the same path would hand this
-    // rank a dead id: only a file written since shortly before this call
-    // counts (rank 0 publishes within seconds of the others reaching here).
-    const time_t not_before = time(nullptr) - 30;
+    const time_t not_before = time(nullptr) - (time_t)(timeout_s > 30 ? timeout_s : 30);
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       struct stat sb;
-      FILE* f = (stat(path.c_str(), &sb) == 0 && sb.st_mtime >= not_before)
-                    ? fopen(path.c_str(), "rb") : nullptr;
+      const bool fresh = stat(path.c_str(), &sb) == 0 && (!token.empty() || sb.st_mtime >= not_before);
+      FILE* f = fresh ? fopen(path.c_str(), "rb") : nullptr;
       if (f) {
-        const size_t got = fread(&id, sizeof(id), 1, f);
+        IdFile got;
+        const size_t n = fread(&got, sizeof(got), 1, f);
         fclose(f);
-        if (got == 1) break;
+        if (n == 1 && !std::memcmp(got.magic, kIdMagic, sizeof(kIdMagic)) &&
+            !std::strncmp(got.token, token.c_str(), sizeof(got.token))) {
+          rec = got;
+          break;
+        }
       }
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > timeout_s) return fail(-2, "rank %d: no unique id at %s after %.0f s", rank, path.c_str(), el);
+      if (el > timeout_s)
+        return fail(-2, "rank %d: no unique id of this job (token '%s') at %s after %.0f s", rank,
+                    token.c_str(), path.c_str(), el);
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
   }
   ncclComm_t c;
-  NCCLC(ncclCommInitRank(&c, world, id, rank));
+  NCCLC(ncclCommInitRank(&c, world, rec.id, rank));
   *comm = c;
   return 0;
 }
@@ -706,6 +737,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   auto buf_ptr = [&](void* base, size_t ld, int b) { return (char*)base + (size_t)b * hB * ld * es; };
   std::vector<std::pair<double, double>> busy, waits;
   double comm_ms = 0, sweep_base_ms = 0;
+  long long n_exch = 0, n_bytes = 0;
   // One sweep: every dependency is an event; the host never waits.
   auto sweep = [&]() -> int {
     std::vector<hipEvent_t> last[4];   // task events on each half since its last exchange
@@ -760,6 +792,8 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
           return -1;
         };
         size_t a0, ln;
+        ++n_exch;
+        for (int i = 0; i < nm; ++i) n_bytes += (long long)msgs[i].n * (long long)es;
         NCCLC(ncclGroupStart());  // direct messages / phase 1
         for (int i = 0; i < nm; ++i) {
           const Msg& M = msgs[i];
@@ -899,9 +933,14 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   int rc = 0;
   p->sweeps = 0;
   p->converged = 0;
-  // underflow floor of the block EVDs (block.hip needs_rotation)
-  if (svdj_set_norm_floor(svdj_norm_floor_value(h->dtype, h->m_pad), h->metric, sa) < 0)
+  // negligible-column floor of the block EVDs (block.hip needs_rotation),
+  // relative to the largest squared column norm: local value, then the max
+  // over ranks (the floor is monotone in that norm)
+  if (svdj_set_norm_floor_scaled(h->dtype, h->m_pad, p->D, 2 * p->B, h->metric, sa) < 0)
     return fail(-100, "norm floor: %s", svdj_hip_last_error());
+  if (P > 1 &&
+      ncclAllReduce(h->metric + 2, h->metric + 2, 1, ncclFloat64, ncclMax, comm, sa) != ncclSuccess)
+    return fail(-200, "norm floor all-reduce failed");
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;
     // ---- stop test: global max convergence value (positive floats order as
@@ -967,6 +1006,8 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   } else if (rc) {
     (void)hipDeviceSynchronize();  // nothing of this call may still run on its buffers
   }
+  p->exchanges = n_exch;
+  p->bytes_sent = n_bytes;
   if (h->timing) {
     p->comm_ms = comm_ms;
     p->exposed_comm_ms = exposed_time(waits, busy);

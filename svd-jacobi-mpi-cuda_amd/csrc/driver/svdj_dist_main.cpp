@@ -42,6 +42,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -421,6 +422,10 @@ int main(int argc, char** argv) {
   if (o.np < 1) o.np = 1;
   if (o.id_file.empty()) o.id_file = "/tmp/svdj_dist_" + std::to_string(getpid()) + ".id";
   std::remove(o.id_file.c_str());
+  // one job token for the ranks forked below (svdj_dist_comm_init accepts
+  // only an id file carrying it)
+  const std::string tok = std::to_string(getpid()) + "-" + std::to_string((long long)time(nullptr));
+  setenv("SVDJ_JOB_TOKEN", tok.c_str(), 1);
   std::fflush(stdout);
   // fork every rank before anything touches the GPU; the parent only waits
   std::vector<pid_t> pids;

@@ -2633,7 +2633,7 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   int sweeps = 0, rc = 0;
   uint32_t hm[2];
   // underflow floor of this solve (metric[2..3])
-  rc = svdj_set_norm_floor(svdj_norm_floor_value(dtype, m_pad), metric, stream);
+  rc = svdj_set_norm_floor_scaled(dtype, m_pad, D, ncols, metric, stream);
   for (int sw = 0; sw < max_sweeps && rc >= 0; ++sw) {
     if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
     rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,

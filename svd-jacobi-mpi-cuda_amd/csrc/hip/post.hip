@@ -139,8 +139,10 @@ extern "C" int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int
   return 0;
 }
 
-// metric[2..3] (a double) = the underflow floor of the block EVDs
-// (block.hip needs_rotation): squared norms at or below m realmin / eps.
+// metric[2..3] (a double) = the negligible-column floor of the block EVDs
+// (block.hip needs_rotation).  svdj_norm_floor_value is its scale-relative
+// factor m realmin / eps (times the largest squared column norm, see
+// svdj_set_norm_floor_scaled).
 __global__ void norm_floor_kernel(double v, uint32_t* __restrict__ metric) {
   if (threadIdx.x == 0) *reinterpret_cast<double*>(metric + 2) = v;
 }
@@ -152,6 +154,39 @@ extern "C" double svdj_norm_floor_value(int dtype, int m) {
 
 extern "C" int svdj_set_norm_floor(double floor, uint32_t* metric, void* stream) {
   hipLaunchKernelGGL(norm_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, floor, metric);
+  SVDJ_LAUNCH_CHECK();
+  return 0;
+}
+
+// Scale-relative floor (ops/kernels.py norm_floor): metric[2..3] =
+// max(m realmin, m realmin / eps * max_j D[j]) over the n squared norms D,
+// on the device (one workgroup).
+template <typename T>
+__global__ __launch_bounds__(256) void norm_floor_scaled_kernel(const T* __restrict__ D, int n,
+                                                                double fabs_, double frel,
+                                                                uint32_t* __restrict__ metric) {
+  __shared__ double wm[4];
+  double mx = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) mx = fmax(mx, (double)D[i]);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
+    *reinterpret_cast<double*>(metric + 2) = fmax(fabs_, frel * mx);
+  }
+}
+
+extern "C" int svdj_set_norm_floor_scaled(int dtype, int m, const void* D, int n,
+                                          uint32_t* metric, void* stream) {
+  const double tiny = dtype == 1 ? 2.2250738585072014e-308 : 1.1754943508222875e-38;
+  const double fabs_ = (double)m * tiny, frel = svdj_norm_floor_value(dtype, m);
+  if (dtype == 1)
+    hipLaunchKernelGGL(norm_floor_scaled_kernel<double>, dim3(1), dim3(256), 0,
+                       (hipStream_t)stream, (const double*)D, n, fabs_, frel, metric);
+  else
+    hipLaunchKernelGGL(norm_floor_scaled_kernel<float>, dim3(1), dim3(256), 0,
+                       (hipStream_t)stream, (const float*)D, n, fabs_, frel, metric);
   SVDJ_LAUNCH_CHECK();
   return 0;
 }

@@ -88,6 +88,8 @@ typedef struct {
   double comm_ms;             // out (comm_timing): sum of exchange spans
   double exposed_comm_ms;     // out (comm_timing): time some compute stream waited for an
                               // arrival while no task ran on either compute stream
+  long long exchanges;        // out: half exchanges issued by this rank (timing or not)
+  long long bytes_sent;       // out: bytes this rank sent in them (relay hops excluded)
 } svdj_dist_problem;
 
 // Persistent per-rank state for repeated solves of one geometry: workspaces,

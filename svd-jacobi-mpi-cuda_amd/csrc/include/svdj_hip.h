@@ -129,6 +129,10 @@ int svdj_col_norms2(int dtype, const void* A, int m_pad, int lda, int ncols, voi
 // uint32), once per solve.
 double svdj_norm_floor_value(int dtype, int m);
 int svdj_set_norm_floor(double floor, uint32_t* metric, void* stream);
+// Scale-relative floor max(m realmin, m realmin / eps * max D) from the n squared
+// column norms D (device, data type) into metric[2..3].
+int svdj_set_norm_floor_scaled(int dtype, int m, const void* D, int n, uint32_t* metric,
+                               void* stream);
 // sigma[c] = ||a_c||; if scale_u, a_c /= sigma[c] (sigma == 0 columns untouched).
 int svdj_finalize(int dtype, void* A, int m_pad, int lda, int ncols, void* sigma, int scale_u, void* stream);
 

@@ -145,7 +145,8 @@ class DistProblem(C.Structure):
                 ("stream_b", c_void_p), ("stream_comm", c_void_p), ("timeout_s", c_double),
                 ("comm_timing", c_int), ("fault_rank", c_int), ("fault_sweep", c_int),
                 ("handle", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
-                ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double)]
+                ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double),
+                ("exchanges", C.c_longlong), ("bytes_sent", C.c_longlong)]
 
 
 def dist_lib_path() -> Path:

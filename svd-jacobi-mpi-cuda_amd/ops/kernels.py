@@ -90,18 +90,21 @@ def reset_metric(metric: torch.Tensor):
     metric[:2].zero_()  # the floor (set once per solve) stays
 
 
-def norm_floor(dtype: torch.dtype, m: int) -> float:
-    """Underflow floor m realmin / eps of the working type: the block EVDs
-    (block.hip needs_rotation) do not rotate pairs with a squared column norm
-    at or below it -- its products and sums have lost their precision to
-    underflow (LAPACK xGESVJ skips such columns likewise)."""
+def norm_floor(dtype: torch.dtype, m: int, dmax: float = 1.0) -> float:
+    """Negligible-column floor: the block EVDs (block.hip needs_rotation) do
+    not rotate pairs with a squared column norm at or below
+    max(m realmin, m realmin / eps * dmax), dmax the largest squared column
+    norm of the matrix.  The second term is the round-3 floor m realmin / eps
+    taken relative to the matrix's scale, so c A is solved like A (LAPACK
+    xGESVJ prescales A for the same reason); the first keeps columns whose
+    products would be subnormal out whatever the scale."""
     fi = torch.finfo(torch.float64 if dtype == torch.float64 else torch.float32)
-    return m * fi.tiny / fi.eps
+    return max(m * fi.tiny, m * fi.tiny / fi.eps * float(dmax))
 
 
-def set_norm_floor(metric: torch.Tensor, dtype: torch.dtype, m: int):
+def set_norm_floor(metric: torch.Tensor, dtype: torch.dtype, m: int, dmax: float = 1.0):
     """Store :func:`norm_floor` in the metric (once per solve)."""
-    v = norm_floor(dtype, m)
+    v = norm_floor(dtype, m, dmax)
     if metric.device.type == "cpu":
         metric[2] = v
     else:
@@ -383,7 +386,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
     modes = [1] + [0] * (nb - 2)
     hist = []
     metric = new_metric("cpu")
-    set_norm_floor(metric, At.dtype, m_pad)
+    set_norm_floor(metric, At.dtype, m_pad, float(D.max()) if D.numel() else 1.0)
     for _ in range(max_sweeps):
         reset_metric(metric)
         block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric,

@@ -267,7 +267,12 @@ class DistributedBlockJacobi(Solver):
             rV = torch.empty(B, n_v, dtype=dtype, device=dev) if want_v else None
             rD = torch.empty(B, dtype=dtype, device=dev)
         metric = K.new_metric(dev)
-        K.set_norm_floor(metric, dtype, m_pad)
+        # scale of the negligible-column floor: the largest squared column norm
+        # of the whole matrix (one all-reduce at setup)
+        dmax = float(D[:2 * B].max()) if D.numel() else 1.0
+        if comm.distributed:
+            dmax = comm.max_over_ranks(dmax)
+        K.set_norm_floor(metric, dtype, m_pad, dmax)
         comm.barrier()
 
         hist, t_comm, t_total = [], 0.0, 0.0

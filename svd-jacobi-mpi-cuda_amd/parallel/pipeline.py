@@ -357,6 +357,7 @@ class PipelineExecutor:
         self._busy = []      # (start event, end event) per task
         self.bytes_sent = 0
         self.bytes_relayed = 0
+        self.exchanges = 0   # half exchanges issued (counted with or without timing)
         # the simulated communicator models a spread exchange by its time only
         self.exchange = resolve_exchange(exchange, comm.world)
         self.spread = self.exchange == "spread" and getattr(comm, "backend", "") != "sim"
@@ -474,6 +475,7 @@ class PipelineExecutor:
             sends.append((self.Vt[so], dst))
             recvs.append((self.Vt[si], src))
         self.bytes_sent += sum(t.numel() * t.element_size() for t, _ in sends)
+        self.exchanges += 1
         if not comm.distributed:
             raise RuntimeError("exchange on a single rank")
         # from here on (host program order) the half lives in the received buffer
@@ -589,10 +591,15 @@ class PipelineExecutor:
                     t[self._buf(dst)].copy_(t[self._buf(src)])
 
     def comm_summary(self) -> dict:
-        """Exchange timing of every sweep run so far (synchronises)."""
-        out = {"exchanges": len(self._spans), "bytes_sent": int(self.bytes_sent),
-               "exchange": self.exchange, "bytes_relayed": int(self.bytes_relayed)}
-        if not self.timing or self._t0 is None:
+        """Exchange counts and bytes of every sweep run so far; with timing
+        on also the exchange times (synchronises).  The timing fields are
+        absent when timing is off."""
+        out = {"exchanges": int(self.exchanges), "bytes_sent": int(self.bytes_sent),
+               "exchange": self.exchange, "bytes_relayed": int(self.bytes_relayed),
+               "timing": bool(self.timing and self._t0 is not None)}
+        if self.exchange == "spread":
+            out["exchange_choice"] = "spread: model-based default (parallel/spread.py)"
+        if not out["timing"]:
             return out
         torch.cuda.synchronize(self.At.device)
         t0 = self._t0

@@ -59,6 +59,9 @@ def main():
                            "sweeps": [d.sweeps, s_.sweeps],
                            "exchange": [d.info["exchange"], s_.info["exchange"]],
                            "relayed": s_.info["comm"]["bytes_relayed"],
+                           "exchanges": [d.info["comm"]["exchanges"], s_.info["comm"]["exchanges"]],
+                           "timing": [d.info["comm"]["timing"], s_.info["comm"]["timing"]],
+                           "comm_ms_absent": "comm_ms" not in d.info["comm"],
                            "world": comm.world}, f)
         comm.destroy()
         return

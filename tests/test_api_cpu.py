@@ -189,3 +189,29 @@ def test_norm_floor_skips_underflowing_columns(svdj):
     assert not bool(rot[0])                  # the underflowing (2, 3) pair does not
     _, _, rot = R.jacobi_evd(G, 1e-14, 1, floor=0.0)
     assert bool(rot[0])
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-16, 2.0 ** 40])
+def test_block_solve_is_scale_invariant(svdj, scale):
+    """c A solves like A: the negligible-column floor is relative
+    to the matrix's largest squared column norm, so a well-conditioned fp32
+    matrix with entries ~1e-16 is rotated (the round-3 absolute floor m realmin
+    / eps skipped every pair and returned A's normalised columns as U)."""
+    import torch
+    A = svdj.utils.inputs.random_dense(96, 64, dtype=torch.float64, seed=4).float()
+    ref = torch.linalg.svdvals(A.double())
+    res = svdj.svd(A * scale, method="block", block=32, sort=True)
+    assert res.converged
+    S = res.S.double() / scale
+    assert float(((S - ref).abs() / ref[0]).max()) < 1e-5
+    U = res.U.double()
+    assert float((U.t() @ U - torch.eye(64, dtype=torch.float64)).abs().max()) < 1e-4
+
+
+def test_norm_floor_relative_to_scale(svdj):
+    import torch
+    K = svdj.ops.kernels
+    fi = torch.finfo(torch.float32)
+    assert K.norm_floor(torch.float32, 100, 1.0) == 100 * fi.tiny / fi.eps
+    assert K.norm_floor(torch.float32, 100, 1e-30) == 100 * fi.tiny  # absolute guard
+    assert K.norm_floor(torch.float32, 100, 4.0) == 4 * 100 * fi.tiny / fi.eps

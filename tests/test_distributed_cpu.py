@@ -73,6 +73,11 @@ def test_spread_exchange_matches_direct(world, m, n, tmp_path):
     assert rep["exchange"] == ["direct", "spread"] and rep["relayed"] > 0, rep
     assert rep["u_diff"] == 0.0 and rep["s_diff"] == 0.0 and rep["v_diff"] == 0.0, rep
     assert rep["sweeps"][0] == rep["sweeps"][1]
+    # exchanges are counted with timing off: per sweep
+    # every rank sends each of its two halves once per round after round 0
+    assert rep["timing"] == [False, False] and rep["comm_ms_absent"], rep
+    per_sweep = 2 * (2 * world - 2)
+    assert rep["exchanges"][0] == rep["exchanges"][1] == per_sweep * rep["sweeps"][0], rep
 
 
 def test_spread_ops_deliver_every_chunk_once():
