@@ -251,6 +251,98 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   }
 }
 
+// fp32 W = 64 cross Gram (GRAM_CROSS / GRAM_QUAD) with coalesced loads.
+// gram_kernel's operand loads follow the MFMA lane map (lane = column): every
+// 16-byte load instruction touches 64 columns, i.e. 64 cache lines.  Here a
+// wave loads its 32-row slab of the pair's 128 columns with lanes along the
+// rows (8 lanes x 16 B = one 128-byte column segment, 8 columns per
+// instruction), keeps the next slab in flight in registers, and transposes
+// through a wave-private LDS image [column][32 rows + 4 pad] (144-byte
+// stride: conflict-free ds_read_b128 of 4 rows of a column per lane).  The
+// MFMAs and the reduction are gram_kernel's; no barrier inside the row loop.
+constexpr int kGlStride = 36;  // floats per column in the LDS image
+template <int MODE>
+__global__ __launch_bounds__(kGramThreads) void gram_cross_f32_kernel(
+    const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
+    int rows_per_chunk, float* __restrict__ slabs) {
+  static_assert(MODE == GRAM_CROSS || MODE == GRAM_QUAD, "cross Grams only");
+  constexpr int W = 64, SR = 32, WAVES = kGramThreads / SVDJ_WAVE;
+  using M = Mfma<float>;
+  __shared__ float img[WAVES][2 * W * kGlStride];  // 4 x 18 KB; reused for the reduction
+  const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
+  int pi, pj;
+  gram_pair<MODE>(pairs, pair, pi, pj);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(m_pad, r_begin + rows_per_chunk);
+  // loads: instruction j covers columns 8j .. 8j+7 (lane >> 3), rows 4 (lane & 7) ..
+  const int lc = lane >> 3, lr = (lane & 7) * 4;
+  const float* src[2] = {A + (size_t)pi * W * lda, A + (size_t)pj * W * lda};
+  float* im = img[wave];
+  f32x4 ld[16];
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int col = 8 * j + lc;  // 0..127: x block then y block
+      ld[j] = *reinterpret_cast<const f32x4*>(src[col >> 6] + (size_t)(col & 63) * lda + r0 + lr);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      *reinterpret_cast<f32x4*>(im + (8 * j + lc) * kGlStride + lr) = ld[j];
+  };
+  M::acc_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = M::zero();
+  const int c = lane & 31, kg = lane >> 5;
+  int r0 = r_begin + wave * SR;
+  if (r0 < r_end) {
+    gload(r0);
+    lstore();
+  }
+  for (; r0 < r_end; r0 += WAVES * SR) {
+    const int rn = r0 + WAVES * SR;
+    if (rn < r_end) gload(rn);
+    // rows kg*16 + t of column tile ct: 4 x ds_read_b128 per tile
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        v[ct] = *reinterpret_cast<const f32x4*>(im + (ct * 32 + c) * kGlStride + kg * 16 + q4 * 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = M::mfma(v[a][t], v[2 + b][t], acc[a][b]);
+    }
+    if (rn < r_end) lstore();  // after this wave's reads of the image (in-order LDS)
+  }
+  // combine the waves' partial tiles (sequentially, deterministic)
+  __syncthreads();
+  float* red = &img[0][0];
+  for (int i = threadIdx.x; i < W * W; i += kGramThreads) red[i] = 0.0f;
+  __syncthreads();
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < M::NACC; ++e)
+            red[(a * 32 + M::acc_row(e, lane)) * W + b * 32 + c] += acc[a][b][e];
+    }
+    __syncthreads();
+  }
+  float* out = slabs + ((size_t)pair * nchunk + chunk) * (W * W);
+  for (int i = threadIdx.x; i < W * W; i += kGramThreads) out[i] = red[i];
+}
+
 // -------------------------------------------------------------------- evd
 // The EVD of the 2W x 2W pair Gram runs in ONE workgroup per pair, as a
 // cyclic parallel Jacobi (circle-method round robin: W disjoint rotations per
@@ -2187,6 +2279,10 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
     set_error("split-bf16 matrix-core modes need fp32 data");
     return -3;
   }
+  if (sizeof(T) == 4 && W == 64 && lda % 4) {  // gram_cross_f32_kernel's 16-byte loads
+    set_error("fp32 W = 64 needs lda %% 4 == 0, got %d", lda);
+    return -2;
+  }
   c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
   c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
   c.g = make_geometry(W, P, m_pad, V ? n_v : 0, mma);
@@ -2245,7 +2341,7 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     const int b = s & 1;
     const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
     const int32_t* pr1 = pr + 2 * c.P;
-    hipLaunchKernelGGL((gram_kernel<float, 64, GRAM_QUAD>), dim3(3 * c.P, c.g.qgch, 1),
+    hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_QUAD>), dim3(3 * c.P, c.g.qgch, 1),
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.qgrows, c.qslabs);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
@@ -2303,6 +2399,9 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
     else
       hipLaunchKernelGGL((gram_kernel<T, W, GRAM_FULL>), dim3(c.P, c.g.gchunks),
                          dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+  } else if constexpr (sizeof(T) == 4 && W == 64) {  // coalesced loads, LDS transpose
+    hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_CROSS>), dim3(c.P, c.g.gchunks),
+                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   } else {
     hipLaunchKernelGGL((gram_kernel<T, W, GRAM_CROSS>), dim3(c.P, c.g.gchunks, XS),
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
@@ -2669,7 +2768,11 @@ extern "C" int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_p
   hipStream_t st = (hipStream_t)stream;
   const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
   if (dtype == 0 && W == 64) {
-    hipLaunchKernelGGL((gram_kernel<float, 64, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
+    if (lda % 4) {
+      set_error("svdj_gram_cross: lda %d must be a multiple of 4", lda);
+      return -2;
+    }
+    hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
                        0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
   } else if (dtype == 0 && W == 32) {
     hipLaunchKernelGGL((gram_kernel<float, 32, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),

@@ -24,7 +24,8 @@ def main():
                                sys.argv[5])
     comm = Communicator(timeout_s=120)
     dev = comm.device
-    cfg = svdj.SolverConfig(block=W, dtype=torch.float32, chains=chains, comm_timing=True,
+    timing = os.environ.get("SVDJ_TEST_TIMING", "1") == "1"
+    cfg = svdj.SolverConfig(block=W, dtype=torch.float32, chains=chains, comm_timing=timing,
                             precondition="none", progress=True,
                             exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"))
     solver = DistributedBlockJacobi(cfg, comm)
@@ -42,7 +43,8 @@ def main():
         torch.save({"U": res.U.cpu(), "S": res.S.cpu(), "V": res.V.cpu(), "A": A.cpu(),
                     "sweeps": res.sweeps, "converged": res.converged, "history": res.history,
                     "backend": comm.backend, "world": comm.world,
-                    "exchange": res.info.get("exchange"),
+                    "exchange": res.info.get("exchange"), "mma": res.info.get("mma"),
+                    "inner_order": res.info.get("inner_order"),
                     "comm": json.dumps(res.info.get("comm"))}, out)
     comm.destroy()
 

@@ -12,6 +12,7 @@ on the same data; only the cross-stream ordering differs, so any missing
 dependency shows up as a difference), and the solve must be accurate.
 The reference ran its MPI path with 2 ranks (build/runSVDMPICUDA.slurm:4-7).
 """
+import json
 import os
 import socket
 import subprocess
@@ -33,9 +34,10 @@ def _port():
     return p
 
 
-def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=300, exchange="auto"):
+def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=300, exchange="auto",
+         timing=True):
     env = dict(os.environ, SVDJ_SHARED_GPU="1", SVDJ_COMM_BACKEND=backend, OMP_NUM_THREADS="2",
-               SVDJ_TEST_EXCHANGE=exchange)
+               SVDJ_TEST_EXCHANGE=exchange, SVDJ_TEST_TIMING="1" if timing else "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(n), str(W),
            str(chains), mode, str(out)]
@@ -71,6 +73,24 @@ def test_rccl_matches_gloo_bitwise(P, tmp_path):
         assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
     _check_accuracy(r)
     assert '"comm_ms"' in r["comm"] and '"exposed_comm_ms"' in r["comm"], r["comm"]
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_production_default_rccl_matches_gloo(P, tmp_path):
+    """The configuration an 8-GPU node runs by default: W =
+    64, mma auto -> bf16x6 split apply, inner order auto -> cross-only EVD +
+    Q build, exchange auto -> spread (relayed over all peers from 4 ranks),
+    comm timing off; n = 4096 so a half super-block holds 2 W-blocks.  RCCL
+    must equal the host-synchronised gloo run bitwise and be accurate."""
+    r = _run(P, "nccl", tmp_path / "rccl.pt", n=4096, W=64, timing=False, timeout=400)
+    g = _run(P, "gloo", tmp_path / "gloo.pt", n=4096, W=64, timing=False, timeout=400)
+    assert (r["mma"], r["inner_order"], r["exchange"]) == ("bf16x6", "cross", "spread"), r
+    assert r["world"] == P and r["sweeps"] == g["sweeps"], (r["history"], g["history"])
+    for k in ("U", "S", "V"):
+        assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
+    _check_accuracy(r)
+    c = json.loads(r["comm"])
+    assert c["exchanges"] == 2 * (2 * P - 2) * r["sweeps"] and not c["timing"], c
 
 
 def test_rccl_spread_exchange_matches_direct(tmp_path):

@@ -14,13 +14,16 @@ pytestmark = pytest.mark.gpu
 
 def _orth_blocks(nb, W, m, m_pad, seed):
     """nb internally orthogonal W-column blocks (cross steps start from such
-    blocks), column norms graded 1..3, as At (nb*W, m_pad) fp64."""
+    blocks), column norms graded 1..3 and scaled per block (equal norms in
+    two blocks make the first bipartite rotations exact 45-degree ties whose
+    direction is decided by rounding), as At (nb*W, m_pad) fp64."""
     g = torch.Generator().manual_seed(seed)
     A64 = torch.zeros(nb * W, m_pad, dtype=torch.float64)
     A64[:, :m] = torch.rand(nb * W, m, generator=g, dtype=torch.float64) - 0.3
     for b in range(nb):
         q, _ = torch.linalg.qr(A64[b * W:(b + 1) * W, :m].t())
-        A64[b * W:(b + 1) * W, :m] = (q * torch.linspace(1, 3, W, dtype=torch.float64)).t()
+        sc = torch.linspace(1, 3, W, dtype=torch.float64) * (1 + 0.37 * b / nb)
+        A64[b * W:(b + 1) * W, :m] = (q * sc).t()
     return A64
 
 
