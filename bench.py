@@ -82,33 +82,51 @@ def verify_distributed(res, gen, m, n, comm, dtype):
     U = res.U[idx, :m].t().to(dev)
     V = res.V[idx, :n].t().to(dev)
     sig = res.S[idx].to(dev)
-    R = A @ V - U * sig
     gidx = torch.tensor(glob, device=dev, dtype=torch.long)
     # all-gather (global id, column) of every rank's U and V columns
-    cnt = comm.allgather(torch.tensor([len(glob)], dtype=torch.int64, device=dev)).cpu().reshape(-1)
-    mx = int(cnt.max())
-    pad_u = torch.zeros(mx, m, dtype=dtype, device=dev)
-    pad_v = torch.zeros(mx, n, dtype=dtype, device=dev)
-    pad_g = torch.full((mx,), -1, dtype=torch.int64, device=dev)
-    pad_u[:len(glob)], pad_v[:len(glob)], pad_g[:len(glob)] = U.t(), V.t(), gidx
-    Uall, Vall, Gall = comm.allgather(pad_u), comm.allgather(pad_v), comm.allgather(pad_g)
     Ufull = torch.zeros(n, m, dtype=dtype, device=dev)
     Vfull = torch.zeros(n, n, dtype=dtype, device=dev)
-    for h in range(comm.world):
-        c = int(cnt[h])
-        Ufull[Gall[h, :c]] = Uall[h, :c]
-        Vfull[Gall[h, :c]] = Vall[h, :c]
-    del Uall, Vall
-    eye_rows = torch.zeros(len(glob), n, dtype=dtype, device=dev)
-    eye_rows[torch.arange(len(glob), device=dev), gidx] = 1
-    EV = V.t() @ Vfull.t() - eye_rows
-    EU = U.t() @ Ufull.t() - eye_rows
-    parts = torch.stack([R.double().pow(2).sum(), A.double().pow(2).sum() / comm.world,
-                         EV.double().pow(2).sum(), EU.double().pow(2).sum()])
+    if comm.world == 1:  # no gather copies (65536^2: 17 GB per matrix)
+        Ufull[gidx] = U.t()
+        Vfull[gidx] = V.t()
+    else:
+        cnt = comm.allgather(torch.tensor([len(glob)], dtype=torch.int64, device=dev)).cpu().reshape(-1)
+        mx = int(cnt.max())
+        pad_u = torch.zeros(mx, m, dtype=dtype, device=dev)
+        pad_v = torch.zeros(mx, n, dtype=dtype, device=dev)
+        pad_g = torch.full((mx,), -1, dtype=torch.int64, device=dev)
+        pad_u[:len(glob)], pad_v[:len(glob)], pad_g[:len(glob)] = U.t(), V.t(), gidx
+        Uall, Vall, Gall = comm.allgather(pad_u), comm.allgather(pad_v), comm.allgather(pad_g)
+        del pad_u, pad_v
+        for h in range(comm.world):
+            c = int(cnt[h])
+            Ufull[Gall[h, :c]] = Uall[h, :c]
+            Vfull[Gall[h, :c]] = Vall[h, :c]
+        del Uall, Vall
+    # Gram rows in column chunks (65536^2: a whole n x n Gram and its fp64
+    # square would need ~100 GB next to A, U, V)
+    ch = max(1, min(len(glob), (1 << 28) // max(n, 1)))
+    sq = torch.zeros(3, dtype=torch.float64, device=dev)  # residual, V, U
+    mxu = torch.zeros((), dtype=torch.float64, device=dev)
+    mxv = torch.zeros((), dtype=torch.float64, device=dev)
+    for c0 in range(0, len(glob), ch):
+        c1 = min(len(glob), c0 + ch)
+        eye_rows = torch.zeros(c1 - c0, n, dtype=dtype, device=dev)
+        eye_rows[torch.arange(c1 - c0, device=dev), gidx[c0:c1]] = 1
+        Rc = A @ V[:, c0:c1] - U[:, c0:c1] * sig[c0:c1]
+        EV = V[:, c0:c1].t() @ Vfull.t() - eye_rows
+        EU = U[:, c0:c1].t() @ Ufull.t() - eye_rows
+        sq += torch.stack([Rc.double().pow(2).sum(), EV.double().pow(2).sum(),
+                           EU.double().pow(2).sum()])
+        mxu = torch.maximum(mxu, EU.abs().max().double())
+        mxv = torch.maximum(mxv, EV.abs().max().double())
+        del Rc, EV, EU, eye_rows
+    a2 = sum(A[:, c0:c0 + 4096].double().pow(2).sum() for c0 in range(0, n, 4096))
+    parts = torch.stack([sq[0], a2 / comm.world, sq[1], sq[2]])
     parts = comm.allreduce_sum_(parts.to(comm_device(comm, dev))).cpu()
     # largest single entry |u_i^T u_j - delta_ij|: the stop test bounds the
     # final couplings by tol (sqrt(m) eps), so the Frobenius norm grows ~ n tol
-    mx = comm.allgather(torch.stack([EU.abs().max(), EV.abs().max()]).double()).cpu().amax(0)
+    mx = comm.allgather(torch.stack([mxu, mxv])).cpu().amax(0)
     return {"residual_rel": float((parts[0] / parts[1]).sqrt()),
             "orth_v_fro": float(parts[2].sqrt()), "orth_u_fro": float(parts[3].sqrt()),
             "orth_u_max_abs": float(mx[0]), "orth_v_max_abs": float(mx[1]),

@@ -93,7 +93,8 @@ def hip_lib():
             return _hip
         import torch  # noqa: F401  -- load torch's HIP runtime first (shared soname)
 
-        path = _ensure_built("hip")
+        override = os.environ.get("SVDJ_HIP_LIB")  # e.g. an A/B build of the kernels
+        path = Path(override) if override else _ensure_built("hip")
         try:
             lib = C.CDLL(str(path))
         except OSError as e:  # pragma: no cover - GPU box only
