@@ -1599,6 +1599,25 @@ __global__ __launch_bounds__((apply_threads<T, W>())) void apply_kernel(
   }
 }
 
+// A wave-uniform pointer moved to SGPRs (v_readfirstlane), so an access
+// p[lane offset] can use the scalar-base + 32-bit VGPR offset address form.
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+// Element i of a base pointer with a 32-bit byte offset (the caller
+// guarantees i * sizeof(T) < 2^32): for a wave-uniform base the address is
+// SGPR base + 32-bit VGPR offset instead of a 64-bit VGPR address.
+template <typename T>
+__device__ __forceinline__ T& at_u32(T* base, uint32_t i) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + i * (uint32_t)sizeof(T));
+}
+
 // -------------------------------------------------- apply on bf16 matrix cores
 // fp32 data, bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the f32 MFMA rate):
 // every operand is split into NP round-to-nearest bf16 parts,
@@ -1652,7 +1671,7 @@ __device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&q)[NP], const bf16x8
 // identity added back in fp32 the drift is 0.14-0.17 eps against 3 eps for
 // the f32 MFMA (tools/probe_apply.py, profiles/r3_s3/bf16x6).
 template <int W, int NP>
-__global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
+__global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void apply_split_kernel(
     float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
     int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
     const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
@@ -1685,7 +1704,9 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
     r_end = min(n_v, r_begin + rows_v);
   }
   if (r_begin >= r_end) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index through readfirstlane: everything derived from it (own) is
+  // known uniform and stays in SGPRs
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, h = lane >> 5;
   const int ct = wave % NCT, rg = wave / NCT;
   float* const xi = base + (size_t)bi * W * ld;
@@ -1708,23 +1729,30 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
         for (int i = 0; i < NP; ++i) qf[kb][i][e] = p[i];
       }
   }
-  // raw X of this wave's k blocks for rows r .. r+31: x[kbl][e] = X[r + c][ct*32 + 16 kbl + 8h + e]
+  // raw X of this wave's k blocks for rows r .. r+31: x[kbl][e] = X[r + c][ct*32 + 16 kbl + 8h + e].
+  // Column bases are wave-uniform (SGPRs, readfirstlane) with a 32-bit lane
+  // offset, so the loads use the scalar-base address form instead of one
+  // 64-bit VGPR address per column (32 VGPRs the operand prefetch needs).
   const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
   auto load = [&](float (&x)[2][8], int r) {
 #pragma unroll
     for (int kbl = 0; kbl < 2; ++kbl)
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        x[kbl][e] = own[(size_t)(16 * kbl + e) * ld + (lane_off + (uint32_t)r)];
+        x[kbl][e] = at_u32(own + (size_t)(16 * kbl + e) * ld, lane_off + (uint32_t)r);
   };
   const uint32_t st_off = (uint32_t)(4 * h * ld + c);
-  int r0 = r_begin + rg * 32;  // this wave's rows in the current tile
-  float xr[2][8];
-  if (r0 < r_end) load(xr, r0);
-  // tile t covers rows r_begin + t TR .. + TR (the loop condition is uniform
-  // over the workgroup: every wave reaches every barrier)
-  for (int t = 0; r_begin + t * TR < r_end; ++t) {
+  // Loads run two tiles ahead: tile t's raw values are in one register set
+  // while tile t+1's are in flight in the other (the loop is unrolled by two
+  // so both sets are static); tile t+2 is issued into the first set as soon
+  // as tile t's values are in LDS and in the epilogue registers.  One tile of
+  // look-ahead left ~16 KB in flight per workgroup, short of what the HBM
+  // latency under load needs.
+  auto tile = [&](float (&xr)[2][8], int t) -> bool {
+    const int rt = r_begin + t * TR;
+    if (rt >= r_end) return false;  // uniform over the workgroup
     const int buf = t & 1;
+    const int r0 = rt + rg * 32;      // this wave's rows
     const bool mine = r0 < r_end;
     // split this tile's own k blocks into the shared B-fragment image
     if (mine) {
@@ -1756,27 +1784,41 @@ __global__ __launch_bounds__(kApplyThreads) void apply_split_kernel(
         xo[(2 * kbl) * 4 + i] = h ? got : keep;
         xo[(2 * kbl + 1) * 4 + i] = h ? keep : got;
       }
-    const int rn = r0 + TR;
-    if (rn < r_end) load(xr, rn);  // next tile in flight during this tile's MFMAs
+    if (r0 + 2 * TR < r_end) load(xr, r0 + 2 * TR);
     __syncthreads();
     if (mine) {
       f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
+      // B operands of k block kb + 1 are read while kb's MFMAs run
+      bf16x8 xs[NP], xn[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) xs[i] = Xf[buf][rg][0][i][lane];
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb) {
-        bf16x8 xs[NP];
+        if (kb + 1 < NKB) {
 #pragma unroll
-        for (int i = 0; i < NP; ++i) xs[i] = Xf[buf][rg][kb][i][lane];
+          for (int i = 0; i < NP; ++i) xn[i] = Xf[buf][rg][kb + 1][i][lane];
+        }
         // the high-order product in its own accumulator, the small terms in
         // a second one
         lo = mfma_split<NP, 1>(qf[kb], xs, lo);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) xs[i] = xn[i];
       }
       acc += lo;
 #pragma unroll
       for (int e = 0; e < 16; ++e)
-        own[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)r0)] = xo[e] + acc[e];
+        at_u32(own + (size_t)Mfma<float>::acc_row_uni(e) * ld, st_off + (uint32_t)r0) = xo[e] + acc[e];
     }
-    r0 = rn;
+    return true;
+  };
+  float xa[2][8], xb[2][8];
+  const int r0 = r_begin + rg * 32;
+  if (r0 < r_end) load(xa, r0);
+  if (r0 + TR < r_end) load(xb, r0 + TR);
+  for (int t = 0;; t += 2) {
+    if (!tile(xa, t)) break;
+    if (!tile(xb, t + 1)) break;
   }
 }
 

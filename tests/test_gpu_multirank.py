@@ -17,6 +17,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 import torch
@@ -41,12 +42,26 @@ def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=300, excha
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(n), str(W),
            str(chains), mode, str(out)]
-    try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
-    except subprocess.TimeoutExpired as e:  # report what the ranks printed (sweep progress)
-        out_ = (e.stdout or b"")[-3000:], (e.stderr or b"")[-3000:]
-        pytest.fail(f"{backend} P={P} timed out after {timeout} s:\n{out_[0]!r}\n{out_[1]!r}")
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    # P ranks time-sliced on one GPU are slow (P = 8 production default: ~80 s
+    # RCCL + ~190 s gloo), and pytest holds the output of a running test: a
+    # heartbeat line under gpurun_out/ every 30 s shows the run is alive.
+    hb = os.path.join(ROOT, "gpurun_out", "multirank_heartbeat.log")
+    os.makedirs(os.path.dirname(hb), exist_ok=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    t0 = time.monotonic()
+    while True:
+        try:
+            so, se = proc.communicate(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            el = time.monotonic() - t0
+            with open(hb, "a") as f:
+                f.write(f"{time.strftime('%H:%M:%S')} {backend} P={P} n={n} W={W} {el:.0f} s\n")
+            if el > timeout:  # report what the ranks printed (sweep progress)
+                proc.kill()
+                so, se = proc.communicate()
+                pytest.fail(f"{backend} P={P} timed out after {timeout} s:\n{so[-3000:]}\n{se[-3000:]}")
+    assert proc.returncode == 0, so[-3000:] + se[-3000:]
     return torch.load(out, weights_only=False)
 
 
