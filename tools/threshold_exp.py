@@ -34,6 +34,18 @@ nb = n // W
 A = svdj.utils.inputs.random_dense(n, n, dtype=torch.float64, seed=1).float()
 At = A.t().contiguous()
 Vt = torch.eye(n, dtype=torch.float32)
+if a.strategy.startswith("blkpre"):
+    # eigenvectors of the fp32 Gram of each of nblk column super-blocks
+    nblk = int(a.strategy[6:])
+    Q = torch.zeros(n, n)
+    bs = n // nblk
+    for i in range(nblk):
+        sl = slice(i * bs, (i + 1) * bs)
+        _, Qi = torch.linalg.eigh(A[:, sl].t() @ A[:, sl])
+        Q[sl, sl] = Qi.flip(1)
+    At = (A @ Q).t().contiguous()
+    Vt = Q.t().contiguous()
+    a.strategy = "base"
 if a.strategy.startswith("eigpre"):
     # eigenvectors of the fp32 Gram as the starting V (A1 = A Q, V0 = Q)
     G = A.t() @ A
