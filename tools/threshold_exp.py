@@ -4,6 +4,9 @@ Runs the block one-sided Jacobi of the flagship path (W-column blocks, round-rob
 steps, first step of a sweep full, the rest cross-only) with the torch reference
 kernels (ops.reference.block_step) and prints, per sweep, the distribution of
 the per-pair coupling max|c_ij|/sqrt(d_i d_j) and how many pairs were applied.
+Starting points: eigpre / eigpre64 (V0 = eigenvectors of the Gram), blkpreK (eigenvectors
+of K diagonal super-block Grams), rt / rt32 (xGEJSV-style Jacobi on R^T of A = QR without V,
+V recovered by a triangular solve).
 A strategy sets the skip threshold of sweep k from the history; the cost model
 is the number of applied pairs (each costs one read+write of 2W columns of A
 and V) plus one Gram read per pair.
@@ -45,6 +48,15 @@ if a.strategy.startswith("blkpre"):
         Q[sl, sl] = Qi.flip(1)
     At = (A @ Q).t().contiguous()
     Vt = Q.t().contiguous()
+    a.strategy = "base"
+Qqr = None
+if a.strategy.startswith("rt"):
+    # xGEJSV-style: A = QR (fp64), Jacobi on X = R^T without V; V_x by a triangular
+    # solve (rt: fp64 solve, rt32: fp32 solve)
+    Qqr, Rqr = torch.linalg.qr(A.double())
+    At = Rqr.float().contiguous()          # rows of At = columns of X = R^T
+    Vt = None
+    solve32 = a.strategy == "rt32"
     a.strategy = "base"
 if a.strategy.startswith("eigpre"):
     # eigenvectors of the fp32 Gram as the starting V (A1 = A Q, V0 = Q)
@@ -102,7 +114,18 @@ for sw in range(a.max_sweeps):
                       "max": "%.2e" % q["max"]}), flush=True)
     if tau == tol and all(float(o.max()) < tol for o in [offs]):
         break
-Ad, Vd = At.double().t(), Vt.double().t()
+if Qqr is not None:
+    Xf = At.double().t()                   # X_final = X V_x = U_x S
+    Sx = Xf.norm(dim=0)
+    Ux = Xf / Sx
+    if solve32:
+        Vx = torch.linalg.solve_triangular(Rqr.t().float(), Xf.float(), upper=False).double()
+    else:
+        Vx = torch.linalg.solve_triangular(Rqr.t(), Xf, upper=False)   # R^T V_x = X_final
+    Ad = (Qqr @ Vx) * Sx                   # A = Q R = (Q V_x) S U_x^T: columns U_A S
+    Vd = Ux
+else:
+    Ad, Vd = At.double().t(), Vt.double().t()
 S = Ad.norm(dim=0)
 U = Ad / S
 res = float((A.double() - U @ torch.diag(S) @ Vd.t()).norm() / A.double().norm())
