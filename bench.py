@@ -391,6 +391,7 @@ def run_native(a, dtype, work):
     p.exchange = {"auto": 0, "direct": 1, "spread": 2}[a.exchange]
     p.timeout_s = float(timeout)
     p.comm_timing = 1 if a.comm_timing else 0
+    p.progress = 1 if a.progress else 0
     p.fault_rank, p.fault_sweep = -1, -1
     if a.inject_fault:
         p.fault_rank, p.fault_sweep = (int(x) for x in a.inject_fault.split(":"))
@@ -462,8 +463,9 @@ def run_native(a, dtype, work):
                        "engine": "native C++ (libsvdj_dist)", "block_W": W, "super_block_B": B,
                        "mma": mma, "mma_numerics": MMA_NUMERICS.get(mma, ""),
                        "precondition": "none", "chains": 2,
-                       "inner_order": a.inner_order,
-                       "exchange": a.exchange,
+                       "inner_order": {0: "cyclic", 1: "bipartite", 2: "cross"}.get(
+                           int(p.inner_order_used), a.inner_order),
+                       "exchange": {1: "direct", 2: "spread"}.get(int(p.exchange_used), "direct"),
                        "staggered": bool(a.stagger), "root_owned": False},
             "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],

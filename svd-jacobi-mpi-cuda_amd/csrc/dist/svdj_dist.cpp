@@ -459,6 +459,7 @@ struct Watchdog {
 struct svdj_dist_handle_t {
   int rank, world, dtype, W, m_pad, n_v, B, k, hk, hB, has_v, timing;
   bool spread = false;           // exchanges relayed over all links (parallel/spread.py)
+  int io = 0;                    // resolved EVD order of the cross steps (0 cyclic, 1 bip, 2 cross)
   void* relay[2] = {nullptr, nullptr};  // A / V relay chunks, one row per source rank
   size_t relay_n[2] = {0, 0};           // elements per row
   ncclComm_t comm;
@@ -583,6 +584,7 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   };
   // 3 = auto: by the pairs of a cross step (half super-blocks)
   const int io = p->inner_order == 3 ? svdj_choose_inner_order(p->dtype, W, h->hk) : p->inner_order;
+  h->io = io;
   guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
   for (int c = 0; c < 2 && !rc; ++c)
@@ -941,6 +943,9 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   if (P > 1 &&
       ncclAllReduce(h->metric + 2, h->metric + 2, 1, ncclFloat64, ncclMax, comm, sa) != ncclSuccess)
     return fail(-200, "norm floor all-reduce failed");
+  p->inner_order_used = h->io;
+  p->exchange_used = P > 1 ? (h->spread ? 2 : 1) : 0;
+  const auto t_solve = std::chrono::steady_clock::now();
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;
     // ---- stop test: global max convergence value (positive floats order as
@@ -966,6 +971,13 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     memcpy(&mx, &hm[0], sizeof(float));
     if (p->hist) p->hist[sw] = mx;
     p->sweeps = sw + 1;
+    if (p->progress && g == 0) {
+      const double el =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t_solve).count();
+      fprintf(stderr, "[svdj_dist] sweep %d: off %.3e, rotated pairs %u, %.2f s\n", sw + 1,
+              (double)mx, hm[1], el);
+      fflush(stderr);
+    }
     if (p->fault_rank == g && p->fault_sweep == sw + 1) {
       fprintf(stderr, "[svdj_dist] fault injection: rank %d exits after sweep %d\n", g, sw + 1);
       fflush(stderr);

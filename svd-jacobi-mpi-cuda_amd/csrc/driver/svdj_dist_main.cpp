@@ -8,7 +8,7 @@
 //                  [--abs-tol] [--mma auto|native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
 //                  [--exchange auto|direct|spread] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
-//                  [--id-file PATH] [--comm-timing] [--inject-fault RANK:SWEEP] [--keep-going]
+//                  [--id-file PATH] [--comm-timing] [--progress] [--inject-fault RANK:SWEEP] [--keep-going]
 //
 // The launcher forks P ranks before anything touches the GPU (the parent never
 // does) and waits for them; a rank that fails or a job that exceeds --timeout
@@ -61,7 +61,7 @@ struct Opts {
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
   bool dense = false, f32 = false, abs_tol = false, want_v = true, shared = false, verify = false;
-  bool comm_timing = false, keep_going = false;
+  bool comm_timing = false, keep_going = false, progress = false;
   std::string id_file;
 };
 
@@ -172,6 +172,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.hist = hist.data();
   p.timeout_s = o.timeout;
   p.comm_timing = o.comm_timing ? 1 : 0;
+  p.progress = o.progress ? 1 : 0;
   p.fault_rank = o.fault_rank;
   p.fault_sweep = o.fault_sweep;
   // persistent handle: workspaces, pair lists and events once, not per solve
@@ -379,6 +380,7 @@ int main(int argc, char** argv) {
     }
     else if (a == "--id-file") o.id_file = next();
     else if (a == "--comm-timing") o.comm_timing = true;
+    else if (a == "--progress") o.progress = true;
     else if (a == "--keep-going") o.keep_going = true;
     else if (a == "--inject-fault") {
       const std::string v = next();

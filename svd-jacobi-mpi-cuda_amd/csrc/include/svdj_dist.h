@@ -90,6 +90,9 @@ typedef struct {
                               // arrival while no task ran on either compute stream
   long long exchanges;        // out: half exchanges issued by this rank (timing or not)
   long long bytes_sent;       // out: bytes this rank sent in them (relay hops excluded)
+  int progress;               // 1: rank 0 prints one line per sweep on stderr
+  int inner_order_used;       // out: the resolved EVD order (0 cyclic, 1 bipartite, 2 cross)
+  int exchange_used;          // out: the resolved exchange (1 direct, 2 spread)
 } svdj_dist_problem;
 
 // Persistent per-rank state for repeated solves of one geometry: workspaces,

@@ -147,7 +147,8 @@ class DistProblem(C.Structure):
                 ("comm_timing", c_int), ("fault_rank", c_int), ("fault_sweep", c_int),
                 ("handle", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
                 ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double),
-                ("exchanges", C.c_longlong), ("bytes_sent", C.c_longlong)]
+                ("exchanges", C.c_longlong), ("bytes_sent", C.c_longlong),
+                ("progress", c_int), ("inner_order_used", c_int), ("exchange_used", c_int)]
 
 
 def dist_lib_path() -> Path:

@@ -381,3 +381,18 @@ def test_gram_cross_matches_reference(svdj, cuda, W, m, m_pad, rows):
         ref = A64[bi * W:(bi + 1) * W] @ A64[bj * W:(bj + 1) * W].t()
         scale = ref.abs().max().item()
         assert (got[p] - ref).abs().max().item() < 2e-6 * scale * math.sqrt(m / 100)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-16, 2.0 ** 40])
+def test_block_solve_is_scale_invariant_gpu(svdj, cuda, scale):
+    """c A solves like A on the GPU kernels (the negligible-column floor is
+    relative to the largest squared column norm, svdj_set_norm_floor_scaled),
+    at the flagship configuration: W = 64, split-bf16 apply, cross EVD."""
+    A = svdj.utils.inputs.random_dense(1100, 1024, dtype=torch.float64, seed=4).float()
+    ref = torch.linalg.svdvals(A.double())
+    res = svdj.svd((A * scale).to(cuda), method="block", sort=True)
+    assert res.converged and res.info["block"] == 64 and res.info["mma"] == "bf16x6", res.info
+    S = res.S.double().cpu() / scale
+    assert float(((S - ref).abs() / ref[0]).max()) < 2e-6
+    U = res.U.double().cpu()
+    assert float((U.t() @ U - torch.eye(1024, dtype=torch.float64)).abs().max()) < 1e-4
