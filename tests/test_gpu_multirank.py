@@ -94,17 +94,23 @@ def test_rccl_matches_gloo_bitwise(P, tmp_path):
 def test_production_default_rccl_matches_gloo(P, tmp_path):
     """The configuration an 8-GPU node runs by default: W =
     64, mma auto -> bf16x6 split apply, inner order auto -> cross-only EVD +
-    Q build, exchange auto -> spread (relayed over all peers from 4 ranks),
-    comm timing off; n = 4096 so a half super-block holds 2 W-blocks.  RCCL
-    must equal the host-synchronised gloo run bitwise and be accurate."""
+    Q build, exchange auto (RCCL: measured at startup; gloo: spread), comm
+    timing off; n = 4096 so a half super-block holds 2 W-blocks.  RCCL must
+    equal the host-synchronised gloo run bitwise and be accurate."""
     r = _run(P, "nccl", tmp_path / "rccl.pt", n=4096, W=64, timing=False, timeout=400)
     g = _run(P, "gloo", tmp_path / "gloo.pt", n=4096, W=64, timing=False, timeout=400)
-    assert (r["mma"], r["inner_order"], r["exchange"]) == ("bf16x6", "cross", "spread"), r
+    assert (r["mma"], r["inner_order"]) == ("bf16x6", "cross"), r
+    # exchange auto: RCCL times direct vs spread on the job's links at startup
+    # (pipeline.calibrate_exchange; on one shared card direct wins), the
+    # host-synchronised gloo run keeps the model default (spread): the two
+    # must still agree bitwise
+    c = json.loads(r["comm"])
+    assert r["exchange"] in ("direct", "spread") and g["exchange"] == "spread", (r, g["exchange"])
+    assert c["exchange_choice"].startswith("measured at startup"), c
     assert r["world"] == P and r["sweeps"] == g["sweeps"], (r["history"], g["history"])
     for k in ("U", "S", "V"):
         assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
     _check_accuracy(r)
-    c = json.loads(r["comm"])
     assert c["exchanges"] == 2 * (2 * P - 2) * r["sweeps"] and not c["timing"], c
 
 
