@@ -685,6 +685,7 @@ def main():
                 "root_owned": a.root_owned,
                 "exchange": last.info.get("exchange", a.exchange),
                 "quad_steps": bool(last.info.get("quad", False)),
+                "merged_chains": bool(last.info.get("merged_chains", False)),
             },
             "sweeps": sweeps,
             "converged": conv,

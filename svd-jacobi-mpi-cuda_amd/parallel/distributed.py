@@ -27,6 +27,7 @@ reference's layout, or left distributed.
 """
 from __future__ import annotations
 
+import os
 import sys
 import time
 
@@ -312,10 +313,18 @@ class DistributedBlockJacobi(Solver):
 
             if not cfg.stagger:
                 run_pair = None
+        # one rank, no exchanges: the two chains' parallel tasks merged into
+        # single launches (PipelineExecutor.run_merged), opt-in SVDJ_MERGE_CHAINS=1.
+        # Measured (profiles/r4_merge): 16384^2 -6 % per sweep but one more
+        # noise-level sweep (4.87 vs 4.94 s), 8192^2 +10 %, 4096^2 -8 %.
+        merged = (pipelined and not comm.distributed and dev.type == "cuda"
+                  and os.environ.get("SVDJ_MERGE_CHAINS", "0") == "1" and not quad)
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
-                if pipelined:
+                if pipelined and merged:
+                    ex.run_merged(splan, run_steps)
+                elif pipelined:
                     t_comm += ex.run(splan, run_steps, phys, run_pair)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
@@ -358,7 +367,7 @@ class DistributedBlockJacobi(Solver):
         sync()
         t_total = time.perf_counter() - t0
         info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
-                "inner_order": inner, "quad": quad,
+                "inner_order": inner, "quad": quad, "merged_chains": bool(pipelined and merged),
                 "exchange": ex.exchange if pipelined else "direct",
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
         if pipelined and P > 1:

@@ -457,6 +457,30 @@ class PipelineExecutor:
     def _event(self):
         return torch.cuda.Event(enable_timing=self.timing)
 
+    def run_merged(self, plan: SweepPlan, run_steps) -> float:
+        """One sweep on ONE rank (no exchanges) with the two chains merged:
+        the parallel task pairs of the plan (rr0 + rr1, T00 + T11, T01 + T10;
+        ``issue_groups``) become single launches of twice the pairs per step
+        on the caller's stream.  Same block pairs in the same step order as
+        :meth:`run` (the sweep count is the two-chain plan's), but every
+        step's Gram, EVD, Q build and apply cover both chains: the EVD latency
+        is paid once per step instead of being left to the other chain to
+        hide (on one GPU a 64-pair step alone took 636-655 us, the two
+        overlapped chains 678 us per 64 pairs; profiles/r4_steps)."""
+        if self.comm.distributed:
+            raise RuntimeError("run_merged is the single-rank issue")
+        index = {id(it): i for i, it in enumerate(plan.items)}
+        for it in issue_groups(plan.items, True):
+            tasks = it if isinstance(it, tuple) else (it,)
+            if len(tasks) == 2 and list(tasks[0].modes) == list(tasks[1].modes) and \
+                    tasks[0].pairs.shape == tasks[1].pairs.shape:
+                pairs = torch.cat([self._pairs(index[id(t)], t) for t in tasks], dim=1)
+                run_steps(pairs.contiguous(), tasks[0].modes, 0)
+                continue
+            for t in tasks:
+                run_steps(self._pairs(index[id(t)], t), t.modes, 0)
+        return 0.0
+
     def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
         steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
