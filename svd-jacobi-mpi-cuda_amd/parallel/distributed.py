@@ -317,15 +317,16 @@ class DistributedBlockJacobi(Solver):
         # single launches (PipelineExecutor.run_merged), opt-in SVDJ_MERGE_CHAINS=1.
         # Measured (profiles/r4_merge): 16384^2 -6 % per sweep but one more
         # noise-level sweep (4.87 vs 4.94 s), 8192^2 +10 %, 4096^2 -8 %.
-        merged = (pipelined and not comm.distributed and dev.type == "cuda"
+        merged = (pipelined and dev.type == "cuda"
                   and os.environ.get("SVDJ_MERGE_CHAINS", "0") == "1" and not quad)
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
-                if pipelined and merged:
+                if pipelined and merged and not comm.distributed:
                     ex.run_merged(splan, run_steps)
                 elif pipelined:
-                    t_comm += ex.run(splan, run_steps, phys, run_pair)
+                    t_comm += ex.run(splan, run_steps, phys, None if merged else run_pair,
+                                     merge=merged)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:

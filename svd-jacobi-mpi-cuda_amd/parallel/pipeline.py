@@ -423,7 +423,8 @@ class PipelineExecutor:
         self.exchanges = 0   # half exchanges issued (counted with or without timing)
         # the simulated communicator models a spread exchange by its time only
         self.exchange_choice = None
-        if exchange == "auto" and comm.world >= 4 and self.stream_ordered:
+        if (exchange == "auto" and comm.world >= 4 and self.stream_ordered
+                and getattr(comm, "backend", "") != "sim"):
             # RCCL from 4 GPUs: time both exchanges on this node's links once
             # (first tournament round, the real half-buffer sizes) and keep the
             # faster; the data delivered is bitwise the same either way
@@ -481,7 +482,7 @@ class PipelineExecutor:
                 run_steps(self._pairs(index[id(t)], t), t.modes, 0)
         return 0.0
 
-    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None) -> float:
+    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None, merge: bool = False) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
         steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
         independent chains staggered, ``a``/``b`` = (pairs, modes, slot,
@@ -504,10 +505,10 @@ class PipelineExecutor:
         t_comm = 0.0
         halves_done = {}
         index = {id(it): i for i, it in enumerate(plan.items)}
-        groups = self._groups.get(id(plan))
+        groups = self._groups.get((id(plan), merge))
         if groups is None:
-            groups = issue_groups(plan.items, run_pair is not None)
-            self._groups[id(plan)] = groups
+            groups = issue_groups(plan.items, run_pair is not None or merge)
+            self._groups[(id(plan), merge)] = groups
         for it in groups:
             if isinstance(it, Send):
                 tc = time.perf_counter()
@@ -537,7 +538,21 @@ class PipelineExecutor:
                         st = self._event()
                         st.record(s)
                         starts.append(st)
-            if len(tasks) == 2:
+            if len(tasks) == 2 and merge and list(tasks[0].modes) == list(tasks[1].modes) \
+                    and pairs[0].shape == pairs[1].shape:
+                # both tasks as ONE launch per step on the first task's stream,
+                # after the second task's dependencies too (SVDJ_MERGE_CHAINS=1)
+                a, b = tasks
+                sa, sb = self.streams[a.stream], self.streams[b.stream]
+                joined = self._event()
+                joined.record(sb)
+                sa.wait_event(joined)
+                with torch.cuda.stream(sa):
+                    run_steps(torch.cat(pairs, dim=1).contiguous(), a.modes, a.stream)
+                done = self._event()
+                done.record(sa)
+                sb.wait_event(done)
+            elif len(tasks) == 2:
                 a, b = tasks
                 run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
                          (pairs[1], b.modes, b.stream, self.streams[b.stream]))
