@@ -118,3 +118,16 @@ def test_bench_native_engine_matches_python_engine(tmp_path):
     assert nat["sweeps"] == py["sweeps"] and nat["converged"]
     assert nat["accuracy"]["residual_rel"] < 1e-5
     assert abs(nat["accuracy"]["residual_rel"] - py["accuracy"]["residual_rel"]) < 1e-9
+
+
+def test_bench_rank_plan_simulation(tmp_path):
+    """bench.py --simulate-P 4: rank 0's plan of a 4-GPU job on one GPU (the
+    sim communicator: exchanges as device copies, no exchange calibration)
+    prints its ms-per-sweep JSON line."""
+    js = tmp_path / "sim.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--simulate-P", "4",
+                        "--n", "2048", "--sim-sweeps", "1", "--json-out", str(js)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["unit"] == "ms/sweep" and d["simulated_P"] == 4 and d["value"] > 0, d
