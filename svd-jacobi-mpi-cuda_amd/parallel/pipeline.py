@@ -349,17 +349,21 @@ def calibrate_exchange(comm, tour, shapes, dtype, dev, reps: int = 3):
         "spread": [([tensor(o) for o in ops.p1_send], [tensor(o) for o in ops.p1_recv]),
                    ([tensor(o) for o in ops.p2_send], [tensor(o) for o in ops.p2_recv])],
     }
+    def sync():
+        if torch.device(dev).type == "cuda":
+            torch.cuda.synchronize(dev)
+
     times = {}
     for name, phases in variants.items():
         best = float("inf")
         for it in range(reps + 1):
             comm.barrier()
-            torch.cuda.synchronize(dev)
+            sync()
             t0 = time.perf_counter()
             for ps, pr in phases:
                 for w in comm.isendrecv(ps, pr):
                     w.wait()
-            torch.cuda.synchronize(dev)
+            sync()
             dt = comm.max_over_ranks(time.perf_counter() - t0)
             if it:
                 best = min(best, dt)

@@ -44,6 +44,23 @@ def main():
                 json.dump({"ok_ranks": float(t[0]), "world": comm.world}, f)
         comm.destroy()
         return
+    if mode == "calib":  # startup exchange calibration: same choice on every rank, data intact
+        from svdj.parallel.pipeline import calibrate_exchange
+        from svdj.parallel.schedule import tournament
+        tour = tournament(comm.world)
+        choice, summary = calibrate_exchange(comm, tour, [(8, 300), (8, 256)], torch.float64,
+                                             torch.device("cpu"), reps=1)
+        flag = torch.tensor([1.0 if choice == "spread" else 0.0], dtype=torch.float64)
+        import torch.distributed as dist
+        lo, hi = flag.clone(), flag.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if comm.rank == 0:
+            with open(out, "w") as f:
+                json.dump({"choice": choice, "summary": summary, "agree": float(lo[0]) == float(hi[0]),
+                           "world": comm.world}, f)
+        comm.destroy()
+        return
     if mode == "exchcmp":  # spread (relayed over all links) vs direct exchange: same bits
         got = {}
         for ex in ("direct", "spread"):

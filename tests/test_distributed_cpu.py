@@ -80,6 +80,17 @@ def test_spread_exchange_matches_direct(world, m, n, tmp_path):
     assert rep["exchanges"][0] == rep["exchanges"][1] == per_sweep * rep["sweeps"][0], rep
 
 
+@pytest.mark.parametrize("world", [4, 5])
+def test_exchange_calibration_agrees_across_ranks(world, tmp_path):
+    """pipeline.calibrate_exchange (exchange auto on RCCL from 4 GPUs) over
+    gloo: both exchange variants of the first tournament round run to
+    completion (no op mismatch in the relayed phases) and every rank
+    reaches the same decision."""
+    rep = _run(world, 0, 0, 0, tmp_path, mode="calib")
+    assert rep["world"] == world and rep["agree"], rep
+    assert rep["choice"] in ("direct", "spread") and rep["summary"].startswith("measured"), rep
+
+
 def test_spread_ops_deliver_every_chunk_once():
     """Simulate the two phases of spread_ops for every rank of every
     tournament round at P = 3..8: each directed pair's sends and receives
