@@ -264,12 +264,15 @@ constexpr int kGlStride = 36;  // floats per column in the LDS image
 template <int MODE>
 __global__ __launch_bounds__(kGramThreads) void gram_cross_f32_kernel(
     const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
-    int rows_per_chunk, float* __restrict__ slabs) {
+    int rows_per_chunk, float* __restrict__ slabs, int rev) {
   static_assert(MODE == GRAM_CROSS || MODE == GRAM_QUAD, "cross Grams only");
   constexpr int W = 64, SR = 32, WAVES = kGramThreads / SVDJ_WAVE;
   using M = Mfma<float>;
   __shared__ float img[WAVES][2 * W * kGlStride];  // 4 x 18 KB; reused for the reduction
-  const int pair = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
+  // rev: row chunks dispatched last-first (the most recently written rows
+  // of the previous apply first, while they may still sit in the Infinity Cache)
+  const int pair = blockIdx.x, nchunk = gridDim.y,
+            chunk = rev ? nchunk - 1 - (int)blockIdx.y : (int)blockIdx.y;
   int pi, pj;
   gram_pair<MODE>(pairs, pair, pi, pj);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1674,7 +1677,7 @@ template <int W, int NP>
 __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void apply_split_kernel(
     float* __restrict__ A, int lda, int a_chunks, int rows_a, int m_pad, float* __restrict__ V,
     int ldv, int rows_v, int n_v, const int32_t* __restrict__ pairs,
-    const float* __restrict__ Qall, const int32_t* __restrict__ skip) {
+    const float* __restrict__ Qall, const int32_t* __restrict__ skip, int vfirst) {
   constexpr int N = 2 * W;
   constexpr int NCT = N / 32;                   // output column tiles
   constexpr int NKB = N / 16;                   // 16-deep k blocks
@@ -1688,7 +1691,11 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
   const int pair = blockIdx.x;
   if (skip[pair]) return;
   const int bi = pairs[2 * pair], bj = pairs[2 * pair + 1];
-  int chunk = blockIdx.y;
+  // vfirst: V's row chunks dispatched before A's, so A's rows are the most
+  // recently written when the next step's Gram reads them
+  const int vch = gridDim.y - a_chunks;
+  int chunk = vfirst ? (blockIdx.y < (unsigned)vch ? a_chunks + (int)blockIdx.y : (int)blockIdx.y - vch)
+                     : (int)blockIdx.y;
   float* base;
   int ld, r_begin, r_end;
   if (chunk < a_chunks) {
@@ -2223,8 +2230,13 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // With the split-bf16 apply, steps of >= 32 pairs want ~256 (1 GPU 16384^2
   // 4.94 -> 4.84 s, 8192^2 674 -> 659 ms, P=2 plan 165.8 -> 163.5 ms per sweep);
   // the P=4 plan (16 pairs) is 6 % slower at 256 (profiles/r3_s3/gram).
+  // Steps of >= 64 pairs keep the 64-pair chunking (4 row chunks): a merged
+  // one-GPU step (two chains' 64-pair steps in one launch, pipeline.py
+  // run_merged) then sums every pair's Gram exactly as the two chains do, so
+  // the solve is bitwise the two-chain one (same sweeps).
   const int gram_target = P >= 32 ? 256 : 512;
   int want = (gram_target + P - 1) / P;
+  if (P >= 64 && want < 4) want = 4;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.grows = round_up((m_pad + g.gchunks - 1) / g.gchunks, 128);
@@ -2384,7 +2396,7 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
     const int32_t* pr1 = pr + 2 * c.P;
     hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_QUAD>), dim3(3 * c.P, c.g.qgch, 1),
-                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.qgrows, c.qslabs);
+                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.qgrows, c.qslabs, 0);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
                        pr, c.qslabs, c.g.qgch, c.D, c.rec, c.nsteps, c.skip1[b], (float)tol,
@@ -2422,6 +2434,20 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
 
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
+// Dispatch order of the row chunks (SVDJ_STREAM_ORDER, bit 0: cross Gram
+// chunks last-first, bit 1: the apply's V chunks before A's).
+// Default 2: V first, so A -- which the next step's Gram reads -- holds the
+// most recently written lines (single-stream 16384^2 step 642 -> 614 us,
+// bitwise the same result; neutral with two concurrent chains).
+static int stream_order() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SVDJ_STREAM_ORDER");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
+}
+
 template <typename T, int W>
 static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, int max_inner,
                            uint32_t* metric, int mma) {
@@ -2443,7 +2469,8 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
                          dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
   } else if constexpr (sizeof(T) == 4 && W == 64) {  // coalesced loads, LDS transpose
     hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_CROSS>), dim3(c.P, c.g.gchunks),
-                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
+                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs,
+                       stream_order() & 1);
   } else {
     hipLaunchKernelGGL((gram_kernel<T, W, GRAM_CROSS>), dim3(c.P, c.g.gchunks, XS),
                        dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.grows, c.slabs);
@@ -2513,11 +2540,11 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
       if (mma == 1)
         hipLaunchKernelGGL((apply_split_kernel<W, 3>), grid, dim3(kApplyThreads), 0, c.st, c.A,
                            c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
-                           pr, c.Qb[b], c.skipb[b]);
+                           pr, c.Qb[b], c.skipb[b], (stream_order() >> 1) & 1);
       else
         hipLaunchKernelGGL((apply_split_kernel<W, 2>), grid, dim3(kApplyThreads), 0, c.st, c.A,
                            c.lda, c.g.a_chunks, c.g.rows_a, c.m_pad, c.V, c.ldv, c.g.rows_v, nv,
-                           pr, c.Qb[b], c.skipb[b]);
+                           pr, c.Qb[b], c.skipb[b], (stream_order() >> 1) & 1);
       SVDJ_LAUNCH_CHECK();
       return 0;
     }
@@ -2815,7 +2842,7 @@ extern "C" int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_p
       return -2;
     }
     hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
-                       0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
+                       0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs, 0);
   } else if (dtype == 0 && W == 32) {
     hipLaunchKernelGGL((gram_kernel<float, 32, GRAM_CROSS>), dim3(P, nchunk, 1), dim3(kGramThreads),
                        0, st, (const float*)A, lda, m_pad, pairs, rows_per_chunk, (float*)slabs);
@@ -2852,16 +2879,16 @@ extern "C" int svdj_apply_q(int dtype, int W, int mma, void* X, int rows, int ld
   int rc = 0;
   if (dtype == 0 && mma == 1 && W == 64)
     hipLaunchKernelGGL((apply_split_kernel<64, 3>), grid, blk, 0, st, (float*)X, ld, chunks,
-                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2, 0);
   else if (dtype == 0 && mma == 1 && W == 32)
     hipLaunchKernelGGL((apply_split_kernel<32, 3>), grid, blk, 0, st, (float*)X, ld, chunks,
-                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2, 0);
   else if (dtype == 0 && mma == 2 && W == 64)
     hipLaunchKernelGGL((apply_split_kernel<64, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
-                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2, 0);
   else if (dtype == 0 && mma == 2 && W == 32)
     hipLaunchKernelGGL((apply_split_kernel<32, 2>), grid, blk, 0, st, (float*)X, ld, chunks,
-                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);
+                       rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2, 0);
   else if (dtype == 0 && mma == 0 && W == 64)
     hipLaunchKernelGGL((apply_kernel<float, 64>), grid, dim3(apply_threads<float, 64>()), 0, st, (float*)X, ld, chunks,
                        rows_chunk, rows, (float*)nullptr, 0, 0, 0, dbuf, (const float*)Q, dbuf + 2);

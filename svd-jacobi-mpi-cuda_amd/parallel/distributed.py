@@ -313,12 +313,17 @@ class DistributedBlockJacobi(Solver):
 
             if not cfg.stagger:
                 run_pair = None
-        # one rank, no exchanges: the two chains' parallel tasks merged into
-        # single launches (PipelineExecutor.run_merged), opt-in SVDJ_MERGE_CHAINS=1.
-        # Measured (profiles/r4_merge): 16384^2 -6 % per sweep but one more
-        # noise-level sweep (4.87 vs 4.94 s), 8192^2 +10 %, 4096^2 -8 %.
-        merged = (pipelined and dev.type == "cuda"
-                  and os.environ.get("SVDJ_MERGE_CHAINS", "0") == "1" and not quad)
+        # One rank, no exchanges, >= 64 pairs per chain step: the two chains'
+        # parallel tasks merged into single launches of 128+ pairs
+        # (PipelineExecutor.run_merged) -- bitwise the two-chain solve (the
+        # Gram keeps the 64-pair chunking), the EVD latency paid once per step
+        # (profiles/r4_merge).  Smaller steps keep the overlapped chains
+        # (8192^2: 32 pairs per chain, merged +10 %).  SVDJ_MERGE_CHAINS=0/1
+        # overrides; with exchanges merging was slower at every P.
+        env_merge = os.environ.get("SVDJ_MERGE_CHAINS")
+        merged = (pipelined and dev.type == "cuda" and not quad and
+                  (env_merge == "1" if env_merge is not None
+                   else (not comm.distributed and k // 2 >= 64)))
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
