@@ -2562,10 +2562,13 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
 //      1 = fp32 data on bf16 MFMA, 3-way split (fp32-level accuracy),
 //      2 = fp32 data on bf16 MFMA, 2-way split (~2^-17 accuracy, fast mode).
 // Both split modes run in delta form, Y = X + X (Q - I) (apply_split_kernel).
-// Measured on MI355X (bench.py accuracy block, profiles/r3_s3/bf16x6): mode 1
-// matches the f32 MFMA path in residual, U/V orthogonality and sigma error at
-// 512..16384 and is 12-23 % faster per sweep for W = 64, so it is the fp32
-// default there (svdj_choose_mma).
+// Measured on MI355X (bench.py accuracy block, profiles/r3_s3/bf16x6,
+// profiles/r4_accuracy): mode 1 matches the f32 MFMA path in U/V orthogonality
+// and sigma error (16384^2: 2.43e-7 both), its residual is 1.37-1.55e-5 vs
+// 1.03-1.05e-5, and it is 12-23 % faster per sweep for W = 64, so it is the
+// fp32 default there (svdj_choose_mma).  Deferring V's rotation to a side
+// stream (it is not needed by the next Gram) was measured neutral on one
+// stream and 22 % slower with two chains (8192^2, round 4): not kept.
 template <typename T, int W>
 static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inner,
                          uint32_t* metric, int mma) {
