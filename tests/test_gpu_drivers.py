@@ -131,3 +131,26 @@ def test_bench_rank_plan_simulation(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["unit"] == "ms/sweep" and d["simulated_P"] == 4 and d["value"] > 0, d
+
+
+def test_merged_issue_is_bitwise_the_two_chain_solve(svdj, cuda, monkeypatch):
+    """One GPU, 64 pairs per chain step (16384 columns, W = 64): the merged
+    128-pair launches (PipelineExecutor.run_merged, the default there) give
+    bitwise the two-chain result -- same pairs in the same step order and the
+    Gram keeps the 64-pair row chunking.  One sweep of a 16384 x 16384 input."""
+    from svdj.parallel import Communicator, DistributedBlockJacobi
+
+    comm = Communicator(device=cuda, init=False)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    A = torch.rand(16384, 16384, generator=g, device=cuda)
+    out = {}
+    for merge in ("1", "0"):
+        monkeypatch.setenv("SVDJ_MERGE_CHAINS", merge)
+        cfg = svdj.SolverConfig(dtype=torch.float32, block=64, max_sweeps=1)
+        res = DistributedBlockJacobi(cfg, comm).solve(A)
+        assert res.info["merged_chains"] == (merge == "1"), res.info
+        out[merge] = (res.U.clone(), res.S.clone(), res.V.clone(), list(res.history))
+        del res
+    for i in range(3):
+        assert torch.equal(out["1"][i], out["0"][i])
+    assert out["1"][3] == out["0"][3]
