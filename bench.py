@@ -392,6 +392,7 @@ def run_native(a, dtype, work):
     p.timeout_s = float(timeout)
     p.comm_timing = 1 if a.comm_timing else 0
     p.progress = 1 if a.progress else 0
+    p.stop_rule = K.STOP_RULES[a.stop_rule]
     p.fault_rank, p.fault_sweep = -1, -1
     if a.inject_fault:
         p.fault_rank, p.fault_sweep = (int(x) for x in a.inject_fault.split(":"))
@@ -417,18 +418,19 @@ def run_native(a, dtype, work):
                   file=sys.stderr, flush=True)
             os._exit(3)
         check(rc, "svdj_dist_solve")
-        return p.sweeps, bool(p.converged)
+        return p.sweeps, int(p.converged)
 
     for _ in range(a.warmup):
         one()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sweeps, conv = [], True
+    sweeps, conv, reasons = [], True, set()
     for _ in range(a.steps):
         sw, cv = one()
         sweeps.append(sw)
-        conv = conv and cv
+        conv = conv and cv > 0
+        reasons.add({1: "no_rotation", 2: "second_order"}.get(cv, "not_converged"))
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
@@ -466,8 +468,10 @@ def run_native(a, dtype, work):
                        "inner_order": {0: "cyclic", 1: "bipartite", 2: "cross"}.get(
                            int(p.inner_order_used), a.inner_order),
                        "exchange": {1: "direct", 2: "spread"}.get(int(p.exchange_used), "direct"),
-                       "staggered": bool(a.stagger), "root_owned": False},
-            "sweeps": sweeps, "converged": conv, "time_to_converge_s": round(ms / 1e3, 4),
+                       "staggered": bool(a.stagger), "root_owned": False,
+                       "stop_rule": a.stop_rule},
+            "sweeps": sweeps, "converged": conv, "stop_reason": sorted(reasons),
+            "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
             "comm": ({"exchanges": int(p.exchanges), "bytes_sent": int(p.bytes_sent),
                       "timing": bool(a.comm_timing),
@@ -543,6 +547,9 @@ def main():
                         "(spread); auto = spread from 4 GPUs")
     p.add_argument("--quad", default="auto", choices=["auto", "on", "off"],
                    help="fused two-step quad block steps (fp32 W=64 split-bf16; auto: off)")
+    p.add_argument("--stop-rule", default="second_order", choices=["second_order", "no_rotation"],
+                   help="also end after a sweep of noise-level rotations (second_order, "
+                        "csrc/include/svdj_stop.h) or only after a sweep without rotations")
     p.add_argument("--simulate-P", type=int, default=0)
     p.add_argument("--simulate-rank", type=int, default=0)
     p.add_argument("--sim-sweeps", type=int, default=3)
@@ -570,7 +577,7 @@ def main():
                             stagger=bool(a.stagger), precondition=a.precondition,
                             inner_order=a.inner_order,
                             progress=a.progress, comm_timing=a.comm_timing, exchange=a.exchange,
-                            quad=a.quad)
+                            quad=a.quad, stop_rule=a.stop_rule)
     if a.inject_fault:
         r_, s_ = (int(x) for x in a.inject_fault.split(":"))
         cfg.extra["fault_exit"] = (r_, s_)
@@ -620,12 +627,13 @@ def main():
     t0 = time.perf_counter()
     # Only the last solve's outputs are kept (earlier ones are released as the
     # next solve starts); sweeps / convergence / flops are accumulated as scalars.
-    sweeps, conv, flops, last = [], True, 0.0, None
+    sweeps, conv, flops, last, reasons = [], True, 0.0, None, set()
     for _ in range(a.steps):
         last = None
         last = one()
         sweeps.append(last.sweeps)
         conv = conv and last.converged
+        reasons.add(last.info.get("stop_reason") or "not_converged")
         flops += last.info["flops"]
     comm.barrier()
     torch.cuda.synchronize()
@@ -642,7 +650,9 @@ def main():
             acc = verify_rows(last, gen, m, n, comm, work)
         else:
             acc = verify_distributed(last, gen, m, n, comm, work)
-    if not a.no_verify and want_sigma(a, n) and last.info.get("precondition") != "qr":
+    # sigma vs the fp64 oracle; on the QR path sigma is complete on every rank
+    # (the oracle is svdvals of the whole m x n A)
+    if not a.no_verify and want_sigma(a, n):
         if a.root_owned:
             err = None
             if comm.rank == 0:
@@ -686,9 +696,11 @@ def main():
                 "exchange": last.info.get("exchange", a.exchange),
                 "quad_steps": bool(last.info.get("quad", False)),
                 "merged_chains": bool(last.info.get("merged_chains", False)),
+                "stop_rule": a.stop_rule,
             },
             "sweeps": sweeps,
             "converged": conv,
+            "stop_reason": sorted(reasons),
             "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % h) for h in last.history[-3:]],
             "comm": last.info.get("comm"),

@@ -80,6 +80,11 @@ class SolverConfig:
     # blocks (csrc/hip/block.hip "quad step": Gram-space second-step
     # couplings, one K = 256 apply per two steps).  auto: models.block.choose_quad
     quad: str = "auto"
+    # block path: when a sweep ends the iteration.  second_order: also after
+    # a sweep whose applied rotations were all noise-level (largest coupling
+    # x largest sine, csrc/include/svdj_stop.h); no_rotation: only after a
+    # sweep that rotated nothing (the confirmation sweep)
+    stop_rule: str = "second_order"
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0       # sweeps between checkpoints (0: off)
     extra: dict = field(default_factory=dict)
@@ -94,6 +99,9 @@ class SolverConfig:
             raise ValueError(f"exchange must be auto, direct or spread, got {self.exchange!r}")
         if self.quad not in ("auto", "on", "off"):
             raise ValueError(f"quad must be auto, on or off, got {self.quad!r}")
+        if self.stop_rule not in ("second_order", "no_rotation"):
+            raise ValueError(f"stop_rule must be second_order or no_rotation, "
+                             f"got {self.stop_rule!r}")
 
     def bf16_mode(self, A: torch.Tensor | None = None) -> bool:
         """bf16 problem: bf16 in/out, fp32 master copies of A and V, block
@@ -150,6 +158,9 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--progress", action="store_true", help="print one line per sweep (rank 0)")
     p.add_argument("--quad", default="auto", choices=["auto", "on", "off"],
                    help="fused two-step quad block steps (fp32, W=64, split-bf16 apply)")
+    p.add_argument("--stop-rule", default="second_order", choices=["second_order", "no_rotation"],
+                   help="block path: also stop after a sweep of noise-level rotations "
+                        "(second_order) or only after a sweep without rotations")
     return p
 
 
@@ -161,5 +172,6 @@ def config_from_args(a) -> SolverConfig:
                         checkpoint_every=a.checkpoint_every,
                         progress=bool(getattr(a, "progress", False)),
                         quad=getattr(a, "quad", "auto"),
+                        stop_rule=getattr(a, "stop_rule", "second_order"),
                         **({"inner_order": a.inner_order}
                            if getattr(a, "inner_order", None) else {}))

@@ -99,11 +99,14 @@ struct Task {
 extern "C" const char* svdj_dist_last_error(void) { return g_err; }
 
 // The id file carries a job token next to the RCCL id, so a rank accepts
-// only the file of its own job: SVDJ_JOB_TOKEN (svdj_dist_main --np sets a
-// fresh one before forking) or torchrun's TORCHELASTIC_RUN_ID.  Without a
-// token, a file written within timeout_s before this call is accepted (a
-// crashed job's file younger than that would be taken: launchers without a
-// token remove the file before their own rendezvous, as bench.py does).
+// only the file of its own job attempt: SVDJ_JOB_TOKEN (svdj_dist_main --np
+// sets a fresh one before forking) or torchrun's TORCHELASTIC_RUN_ID joined
+// with TORCHELASTIC_RESTART_COUNT (an elastic restart, or a reused
+// --rdzv-id after a crash, must not pick up the dead attempt's id).  The
+// file's age is checked in every case: with a token it must be younger than
+// timeout_s (a leftover of an older job with the same token is refused),
+// without one younger than 30 s (tokenless launchers start their ranks
+// together and remove the file before their rendezvous, as bench.py does).
 namespace {
 struct IdFile {
   char magic[8];
@@ -115,7 +118,10 @@ std::string job_token() {
   const char* t = std::getenv("SVDJ_JOB_TOKEN");
   if (t && *t) return std::string(t).substr(0, 63);
   const char* r = std::getenv("TORCHELASTIC_RUN_ID");
-  if (r && *r && std::strcmp(r, "none")) return std::string(r).substr(0, 63);
+  if (r && *r && std::strcmp(r, "none")) {
+    const char* c = std::getenv("TORCHELASTIC_RESTART_COUNT");
+    return (std::string(r).substr(0, 48) + "#" + (c && *c ? c : "0")).substr(0, 63);
+  }
   return std::string();
 }
 }  // namespace
@@ -135,11 +141,12 @@ extern "C" int svdj_dist_comm_init(int rank, int world, const char* id_path, dou
     fclose(f);
     if (rename(tmp.c_str(), path.c_str()) != 0) return fail(-1, "cannot publish %s", path.c_str());
   } else {
-    const time_t not_before = time(nullptr) - (time_t)(timeout_s > 30 ? timeout_s : 30);
+    const double window = token.empty() ? 30.0 : (timeout_s > 30 ? timeout_s : 30.0);
+    const time_t not_before = time(nullptr) - (time_t)window;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       struct stat sb;
-      const bool fresh = stat(path.c_str(), &sb) == 0 && (!token.empty() || sb.st_mtime >= not_before);
+      const bool fresh = stat(path.c_str(), &sb) == 0 && sb.st_mtime >= not_before;
       FILE* f = fresh ? fopen(path.c_str(), "rb") : nullptr;
       if (f) {
         IdFile got;
@@ -586,10 +593,10 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   const int io = p->inner_order == 3 ? svdj_choose_inner_order(p->dtype, W, h->hk) : p->inner_order;
   h->io = io;
   guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
-  h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad);
+  h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad, 0);
   for (int c = 0; c < 2 && !rc; ++c)
     if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);
-  if (!rc && hipMalloc((void**)&h->metric, 4 * sizeof(uint32_t)) != hipSuccess)
+  if (!rc && hipMalloc((void**)&h->metric, SVDJ_METRIC_WORDS * sizeof(uint32_t)) != hipSuccess)
     rc = fail(-100, "hipMalloc(metric) failed");
   if (p->exchange < 0 || p->exchange > 2) rc = rc ? rc : fail(-2, "exchange %d (0 auto, 1 direct, 2 spread)", p->exchange);
   h->spread = h->world > 2 && (p->exchange == 2 || (p->exchange == 0 && h->world >= 4));
@@ -746,7 +753,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     hipEvent_t pending[4] = {nullptr, nullptr, nullptr, nullptr};  // arrived, not yet waited
     int halves_sent = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> sp_busy, sp_wait, sp_span;
-    HIPC(hipMemsetAsync(h->metric, 0, 2 * sizeof(uint32_t), sa));
+    if (svdj_reset_metric(h->metric, sa) != 0) return fail(-100, "metric reset failed");
     if (h->timing) HIPC(hipEventRecord(h->ev_t0, sa));
     HIPC(hipEventRecord(h->ev_join, sa));
     HIPC(hipStreamWaitEvent(st[1], h->ev_join, 0));
@@ -948,15 +955,17 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   const auto t_solve = std::chrono::steady_clock::now();
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;
-    // ---- stop test: global max convergence value (positive floats order as
-    // uint32) and total rotated pairs
-    uint32_t hm[2] = {0, 0};
+    // ---- stop test (svdj_stop.h): global max convergence value and largest
+    // applied |sin| (positive floats order as uint32), total rotated pairs
+    uint32_t hm[6] = {0, 0, 0, 0, 0, 0};
     auto reduce = [&]() -> int {
       {
         std::lock_guard<std::mutex> lk(wd.mu);
         if (wd.fired.load()) return fail(-300, "%s", wd.why);
         NCCLC(ncclAllReduce(h->metric, h->metric, 1, ncclUint32, ncclMax, comm, sa));
         NCCLC(ncclAllReduce(h->metric + 1, h->metric + 1, 1, ncclUint32, ncclSum, comm, sa));
+        NCCLC(ncclAllReduce(h->metric + 4, h->metric + 4, 1, ncclUint32, ncclMax, comm, sa));
+        NCCLC(ncclAllReduce(h->metric + 5, h->metric + 5, 1, ncclUint32, ncclSum, comm, sa));
       }
       HIPC(hipMemcpyAsync(hm, h->metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
       return wait_sa();
@@ -967,15 +976,17 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
       break;
     }
     wd.progress();
-    float mx;
+    float mx, ms;
     memcpy(&mx, &hm[0], sizeof(float));
+    memcpy(&ms, &hm[4], sizeof(float));
     if (p->hist) p->hist[sw] = mx;
     p->sweeps = sw + 1;
     if (p->progress && g == 0) {
       const double el =
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t_solve).count();
-      fprintf(stderr, "[svdj_dist] sweep %d: off %.3e, rotated pairs %u, %.2f s\n", sw + 1,
-              (double)mx, hm[1], el);
+      fprintf(stderr,
+              "[svdj_dist] sweep %d: off %.3e, eff sin %.3e, rotated pairs %u, rotations %u, %.2f s\n",
+              sw + 1, (double)mx, (double)ms, hm[1], hm[5], el);
       fflush(stderr);
     }
     if (p->fault_rank == g && p->fault_sweep == sw + 1) {
@@ -983,8 +994,10 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
       fflush(stderr);
       _exit(17);
     }
-    if (hm[1] == 0) {
-      p->converged = 1;
+    const int conv =
+        svdj_sweep_converged_inline(mx, ms, hm[1], hm[5], p->tol, p->tol_mode, p->stop_rule);
+    if (conv) {
+      p->converged = conv;
       break;
     }
   }

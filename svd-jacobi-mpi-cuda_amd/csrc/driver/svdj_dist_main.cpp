@@ -6,7 +6,7 @@
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
 //                  [--abs-tol] [--mma auto|native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
-//                  [--exchange auto|direct|spread] [--no-v]
+//                  [--exchange auto|direct|spread] [--stop-rule second_order|no_rotation] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH] [--comm-timing] [--progress] [--inject-fault RANK:SWEEP] [--keep-going]
 //
@@ -57,6 +57,7 @@ namespace {
 struct Opts {
   int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 3;  // auto
   int exchange = 0;  // auto
+  int stop_rule = 1;  // second_order (svdj_stop.h)
   int fault_rank = -1, fault_sweep = -1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
@@ -166,6 +167,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.mma = o.mma < 0 ? svdj_choose_mma(dtype, W) : o.mma;
   p.inner_order = o.inner;
   p.exchange = o.exchange;
+  p.stop_rule = o.stop_rule;
   p.stream_a = sa;
   p.stream_b = sb;
   p.stream_comm = sc;
@@ -381,6 +383,7 @@ int main(int argc, char** argv) {
     else if (a == "--id-file") o.id_file = next();
     else if (a == "--comm-timing") o.comm_timing = true;
     else if (a == "--progress") o.progress = true;
+    else if (a == "--stop-rule") o.stop_rule = std::string(next()) == "no_rotation" ? 0 : 1;
     else if (a == "--keep-going") o.keep_going = true;
     else if (a == "--inject-fault") {
       const std::string v = next();

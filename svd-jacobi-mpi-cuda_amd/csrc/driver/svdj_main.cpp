@@ -55,7 +55,7 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
   CHECK(hipMalloc(&dV, (size_t)ncols * n_v * sizeof(T)));
   CHECK(hipMalloc(&dD, (size_t)ncols * sizeof(T)));
   CHECK(hipMalloc(&dS, (size_t)ncols * sizeof(T)));
-  CHECK(hipMalloc(&dmetric, 2 * sizeof(uint32_t)));
+  CHECK(hipMalloc(&dmetric, SVDJ_METRIC_WORDS * sizeof(uint32_t)));
   CHECK(hipMemcpy(dA, hA.data(), hA.size() * sizeof(T), hipMemcpyHostToDevice));
   hipStream_t st;
   CHECK(hipStreamCreate(&st));
@@ -72,12 +72,12 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
   int32_t* dsched = nullptr;
   if (svdj_set_identity(dtype, dV, n_v, n_v, ncols, 0, st) < 0) goto fail;
   if (block) {
-    const size_t wsb = svdj_block_workspace_bytes(dtype, W, ncols / W / 2, m_pad);
+    const size_t wsb = svdj_block_workspace_bytes(dtype, W, ncols / W / 2, m_pad, 0);
     CHECK(hipMalloc(&ws, wsb));
     if (svdj_col_norms2(dtype, dA, m_pad, m_pad, ncols, dD, st) < 0) goto fail;
     sweeps = svdj_block_solve(dtype, W, m_pad, dA, m_pad, dV, n_v, n_v, dD, ncols, tol,
                               /*tol_mode relative*/ 0, 1, max_sweeps, inner_order, ws, wsb,
-                              dmetric, hist.data(), mma, st);
+                              dmetric, hist.data(), mma, /*stop_rule second_order*/ 1, st);
   } else {
     const int steps = svdj_sameh_num_steps(n);
     std::vector<int32_t> sched((size_t)steps * (n / 2) * 2);

@@ -24,6 +24,7 @@
 #include "common.hpp"
 #include "evd_deal_tables.hpp"
 #include "svdj_hip.h"
+#include "svdj_stop.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -45,31 +46,16 @@ __host__ __device__ constexpr int round_up(int a, int b) { return (a + b - 1) / 
 //                   A_bj^T A_bj, A_bi^T A_bj), one per blockIdx.z: the
 //                   one-launch form keeps 2W(2W+1)/2 tile accumulators, which
 //                   for fp64 W = 64 exceed the register file.
+// (The cross Grams of a quad step: gram_quad_kernel.)
 // For fp64 W = 64 the cross products are also split over blockIdx.z in XS = 2
 // row halves (x tiles), so accumulators plus the double-buffered loads fit in
 // registers without spilling.
-//       GRAM_QUAD   the cross Grams a quad step needs (see "quad step" below):
-//                   `pairs` holds two steps (s: (a,c),(b,d); s+1: (a,d),(b,c)
-//                   per quad), gridDim.x = 3P: slabs [0, P) are step s's
-//                   pairs, slab P + 4q + r the blocks (a,d), (b,c), (a,b),
-//                   (c,d) of quad q.
-enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2, GRAM_QUAD = 3 };
+enum { GRAM_CROSS = 0, GRAM_FULL = 1, GRAM_SPLIT = 2 };
 
-// (bi, bj) of Gram slab `pair` (see GRAM_QUAD).
+// (bi, bj) of Gram slab `pair`.
 template <int MODE>
 __device__ __forceinline__ void gram_pair(const int32_t* __restrict__ pairs, int pair, int& pi,
                                           int& pj) {
-  if constexpr (MODE == GRAM_QUAD) {
-    const int P = (int)gridDim.x / 3;
-    if (pair >= P) {
-      const int j = pair - P, q = j >> 2, r = j & 3;
-      const int32_t* s0 = pairs + 4 * q;          // (a, c), (b, d)
-      const int32_t* s1 = pairs + 2 * P + 4 * q;  // (a, d), (b, c)
-      pi = r == 0 ? s1[0] : r == 1 ? s1[2] : r == 2 ? s0[0] : s0[1];
-      pj = r == 0 ? s1[1] : r == 1 ? s1[3] : r == 2 ? s0[2] : s0[3];
-      return;
-    }
-  }
   pi = pairs[2 * pair];
   pj = pairs[2 * pair + 1];
 }
@@ -251,7 +237,7 @@ __global__ __launch_bounds__(kGramThreads) void gram_kernel(
   }
 }
 
-// fp32 W = 64 cross Gram (GRAM_CROSS / GRAM_QUAD) with coalesced loads.
+// fp32 W = 64 cross Gram (GRAM_CROSS) with coalesced loads.
 // gram_kernel's operand loads follow the MFMA lane map (lane = column): every
 // 16-byte load instruction touches 64 columns, i.e. 64 cache lines.  Here a
 // wave loads its 32-row slab of the pair's 128 columns with lanes along the
@@ -265,7 +251,7 @@ template <int MODE>
 __global__ __launch_bounds__(kGramThreads) void gram_cross_f32_kernel(
     const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
     int rows_per_chunk, float* __restrict__ slabs, int rev) {
-  static_assert(MODE == GRAM_CROSS || MODE == GRAM_QUAD, "cross Grams only");
+  static_assert(MODE == GRAM_CROSS, "cross Grams only");
   constexpr int W = 64, SR = 32, WAVES = kGramThreads / SVDJ_WAVE;
   using M = Mfma<float>;
   __shared__ float img[WAVES][2 * W * kGlStride];  // 4 x 18 KB; reused for the reduction
@@ -435,6 +421,16 @@ __device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gp
   if (absmode) return fabs(gpq) > tol;
   const double nrm = sqrt(gpp) * sqrt(gqq);
   return nrm > 0.0 && fabs(gpq) > tol * nrm && fmin(gpp, gqq) > floor;
+}
+// Effective sine of a rotation for the second-order stop test
+// (svdj_stop.h): |s| times the larger ratio of the two columns' norms after
+// it (d = squared norms); 0 for no rotation.
+template <typename T>
+__device__ __forceinline__ float eff_sine(T s, T dp, T dq) {
+  if (s == T(0)) return 0.0f;
+  const float a = (float)fabs(dp), b = (float)fabs(dq);
+  const float lo = fminf(a, b), hi = fmaxf(a, b);
+  return lo > 0.0f ? fabsf((float)s) * sqrtf(hi / lo) : 1.0f;
 }
 // The negligible-column floor of this solve (metric[2..3], a double).
 template <typename T>
@@ -945,7 +941,14 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
   }
 
   // ---- prologue: step 0's rotations from the assembled G
+  // second-order stop test (svdj_stop.h): largest effective sine and count
+  // of the rotations this solver lane solved (the final look-ahead rotation
+  // included: conservative)
+  float smax = 0.0f;
+  uint32_t rcount = 0;
   auto publish = [&](int b, int ns, T c, T sn, T t, T dfp, T dsp) {
+    smax = fmaxf(smax, eff_sine(sn, dfp, dsp));
+    rcount += sn != T(0) ? 1u : 0u;
     rcs[b][ns] = T2{c, sn};
     rdd[b][ns] = T2{dfp, dsp};
     if constexpr (sizeof(QT) == sizeof(T)) {
@@ -1088,6 +1091,14 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
     while (!step(std::integral_constant<int, 0>{}) && !step(std::integral_constant<int, 1>{})) {
     }
 
+  if (wave == 0 && any) {  // second-order stop test input (metric[4], [5]; svdj_stop.h)
+    const float sm = wave_max(smax);
+    const uint32_t rc_ = wave_sum(rcount);
+    if (lane == 0) {
+      atomic_max_pos(&metric[4], sm);
+      atomicAdd(&metric[5], rc_);
+    }
+  }
   if (tid == 0) {
     skip[pair] = any ? 0 : 1;
     if (any) atomicAdd(&metric[1], 1u);
@@ -1277,6 +1288,11 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
                 // written at the start of the next phase (steps 0 .. gs-1 are
                 // recorded; the look-ahead rotation solved in the final phase
                 // is never used)
+  // second-order stop test (svdj_stop.h): largest effective sine and count
+  // of the rotations applied (recorded); rse: effective sine of the latest
+  // solved rotation
+  float smax = 0.0f, rse = 0.0f;
+  uint32_t rcount = 0;
   auto solve = [&](T dx, T dy, T g, bool& rot) {
     T c, sn, t;
     rot = rotation_fast(dx, dy, g, tol, absmode, nfloor, c, sn, t);
@@ -1285,9 +1301,12 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     rt = t;
     rdx = dx - t * g;
     rdy = dy + t * g;
+    rse = eff_sine(sn, rdx, rdy);
     pend = rot ? T(0) : g;
   };
   auto record = [&](int step) {
+    smax = fmaxf(smax, rse);
+    rcount += rs != T(0) ? 1u : 0u;
     double c64, s64;
     if constexpr (sizeof(T) == 8) {
       c64 = rc;
@@ -1381,6 +1400,14 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     while (!step(std::integral_constant<int, 0>{}) && !step(std::integral_constant<int, 1>{})) {
     }
 
+  if (wave == 0 && any) {  // second-order stop test input (metric[4], [5]; svdj_stop.h)
+    const float sm = wave_max(smax);
+    const uint32_t rc_ = wave_sum(rcount);
+    if (lane == 0) {
+      atomic_max_pos(&metric[4], sm);
+      atomicAdd(&metric[5], rc_);
+    }
+  }
   if (tid == 0) {
     skip[pair] = any ? 0 : 1;
     nsteps[pair] = gs;
@@ -1836,7 +1863,7 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 // of parallel/schedule.py quad_round_robin / quad_bipartite).  Step s+1's
 // couplings are formed in Gram space instead of from the data:
 //   gram   : the six cross Grams C_ac, C_bd, C_ad, C_bc, C_ab, C_cd in ONE
-//            launch (GRAM_QUAD; each block of the quad is read for three
+//            launch (gram_quad_kernel: each block of the quad read once,
 //            products instead of once per step);
 //   evd 1  : evd_cross_kernel on (a,c), (b,d)  -> rotation records;
 //   T1     : qbuild_quad_kernel<1> -> Q_ac, Q_bd in fp64;
@@ -1846,7 +1873,7 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 //   evd 2  : evd_cross_kernel on (a,d), (b,c) from those couplings;
 //   T      : qbuild_quad_kernel<2> applies the step-(s+1) rotations to the
 //            rows of T1 in fp64: T = T1 T2, the whole 256 x 256 transform;
-//   apply  : [a b c d] <- [a b c d] T once, for A and V (apply_quad_kernel).
+//   apply  : [a b c d] <- [a b c d] T once, for A and V (apply_quad_ts_kernel).
 // The data moves through HBM once per two steps instead of twice, and the
 // apply contracts over K = 256 instead of 128: its split-bf16 MFMAs, no
 // longer waiting on HBM, set the pace.  Numerically it is the two W-block
@@ -2033,168 +2060,303 @@ __global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
   for (int i = 0; i < NP; ++i) dst[i * SVDJ_WAVE] = parts[i];
 }
 
-// [a b c d] <- [a b c d] T for 128 rows of A or V per workgroup, in place,
-// T the quad's 256 x 256 transform, split-bf16 delta form Y = X + X (T - I)
-// as apply_split_kernel (transposed: lane = row, coalesced loads/stores).
-// The workgroup owns ALL 256 output columns of its rows, so reading the
-// inputs and writing the outputs in place cannot race with another
-// workgroup (a two-workgroup split of the columns did: each reads all four
-// blocks).  T does not fit a CU's registers in split form (384 KB), so it is
-// streamed through LDS in K chunks of 32 columns (pre-split by
-// tsplit_kernel), double-buffered with the matching X chunk:
-//   8 waves, wave w owns rows 32 (w >> 1) .. + 32 and output column tiles
-//   4 (w & 1) .. + 3 (128 columns, 4 accumulators);
-//   per chunk: 2 k blocks x 4 tiles x 6 MFMAs per wave, operands by
-//   ds_read_b128 (X split image: [row group][k block][part][lane]);
-//   chunk kc is loaded by the four waves that output column tile kc, which
-//   keep its raw values (moved to accumulator lanes by v_permlane32_swap)
-//   for the epilogue.
-// Quad q's workgroups are placed on XCD group q % 8 (blockIdx % 8), so a
-// group's L2 holds the T of only nq / 8 quads.
-constexpr int kQuadApplyThreads = 512;
-constexpr int kQuadRows = 128;
+// [a b c d] <- [a b c d] T, T-STATIONARY (round 5).  The round-4 apply
+// streamed the 384 KB split T through LDS for every 128-row tile (3.2 GB of T
+// per 64-pair quad step against 2.1 GB of data; 1.71 ms per 128-pair quad
+// step, profiles/r4_quad).  Here a workgroup keeps T in REGISTERS for
+// thousands of rows:
+//   * 8 waves (two per SIMD), wave w owns output column tile w (32 of the
+//     quad's 256 columns) and holds its split T - I slice, 16 k blocks x NP
+//     bf16x8 = 192 VGPRs for NP = 3, for the whole launch;
+//   * the workgroup walks a contiguous range of 32-row tiles of A then V
+//     (every tile all 256 columns: it owns its rows, so in place is safe);
+//   * each wave LDS-DMAs (global_load_lds_dwordx4) its own 32 columns of the
+//     tile two tiles ahead into a wave-private raw image (no VGPRs in
+//     flight), splits them into the shared B-fragment image of the tile
+//     (double-buffered, one barrier per tile), runs 16 k blocks x (1 + 5)
+//     MFMAs (leading product and the small ones in two accumulators, as
+//     apply_split_kernel), and rebuilds its own raw values for the delta-form
+//     epilogue Y = X + X (T - I) from that image (the 3-way split is exact).
+// Work: the active quads (some step-s or step-(s+1) pair rotated) are listed
+// by every wave with ballots over the skip flags (no extra launch, no host
+// sync); nact active quads x S row slices, S = max(1, grid / nact), are dealt
+// to the persistent grid (one workgroup per CU: the LDS is 160 KB).
+constexpr int kQuadTsThreads = 512;
+constexpr int kQuadTsGrid = 256;
 template <int NP>
-__global__ __launch_bounds__(kQuadApplyThreads) void apply_quad_kernel(
-    float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
-    const int32_t* __restrict__ pairs, int nq, const bf16x8* __restrict__ Ts,
-    const int32_t* __restrict__ skip1, const int32_t* __restrict__ skip2, int tpq) {
-  constexpr int W = 64, NKC = 8;
-  constexpr int TCH = 2 * 8 * NP * SVDJ_WAVE;  // T fragments per chunk
-  constexpr int TPT = TCH / kQuadApplyThreads;  // per thread
-  __shared__ bf16x8 Tl[2][TCH];
-  __shared__ bf16x8 Xl[2][4][2][NP][SVDJ_WAVE];
+struct QuadTsLds {
+  static constexpr int S_BYTES = 16 * NP * SVDJ_WAVE * 16;  // split image of a 32-row tile
+  static constexpr int R_BYTES = 8 * 32 * 32 * 4;           // raw tile, wave w at 4 KB * w: [col][row]
+  static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
+};
+static_assert(QuadTsLds<3>::TOTAL <= 163840, "T-stationary quad apply LDS");
 
-  const int L = blockIdx.x;
-  int q, t;
-  if (nq % 8 == 0) {
-    const int g = nq / 8, s = L >> 3;
-    q = (s % g) * 8 + (L & 7);
-    t = s / g;
-  } else {
-    q = L % nq;
-    t = L / nq;
-  }
-  if (t >= tpq) return;
-  if (skip1[2 * q] && skip1[2 * q + 1] && skip2[2 * q] && skip2[2 * q + 1]) return;
-  float* base;
-  int ld, r0;
-  if (t < a_tiles) {
-    base = A;
-    ld = lda;
-    r0 = t * kQuadRows;
-  } else {
-    base = V;
-    ld = ldv;
-    r0 = (t - a_tiles) * kQuadRows;
-  }
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+}
+
+template <int NP>
+__global__ __launch_bounds__(kQuadTsThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
+                     int v_tiles, const int32_t* __restrict__ pairs, int nq,
+                     const bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
+                     const int32_t* __restrict__ skip2) {
+  using L = QuadTsLds<NP>;
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, h = lane >> 5;
-  const int rg = wave >> 1, chh = wave & 1;
-  const int32_t* qp = pairs + 4 * q;  // (a, c), (b, d)
-  // column tile kc (32 columns) of the quad: block kc >> 1 in [a b c d] order
-  auto col_ptr = [&](int kc) -> float* {
-    const int qb = kc >> 1;
-    return base + (size_t)(qp[(qb & 1) * 2 + (qb >> 1)] * W + (kc & 1) * 32) * ld;
+  auto active = [&](int q) -> bool {  // all four flags loaded (no short-circuit branches)
+    if (q >= nq) return false;
+    return (skip1[2 * q] & skip1[2 * q + 1] & skip2[2 * q] & skip2[2 * q + 1]) == 0;
   };
-  const bf16x8* Tq = Ts + (size_t)q * 16 * 8 * NP * SVDJ_WAVE;
-  const uint32_t lane_off = (uint32_t)(8 * h * ld + c);
-  const uint32_t st_off = (uint32_t)(4 * h * ld + c);
-  const int rw = r0 + 32 * rg;  // this wave's rows
+  int nact = 0;
+  for (int b0 = 0; b0 < nq; b0 += SVDJ_WAVE) nact += __popcll(__ballot(active(b0 + lane)));
+  if (nact == 0) return;
+  const int G = (int)gridDim.x;
+  const int S = G / nact > 1 ? G / nact : 1;
+  const int nitems = nact * S, nt = a_tiles + v_tiles;
 
-  float xg[2][8];
-  bf16x8 tg[TPT];
-  float xo[4][16];
-  auto gload = [&](int kc) {
-    if ((kc >> 2) == chh) {  // the four loader waves of this chunk
-      const float* p = col_ptr(kc);
-#pragma unroll
-      for (int kbl = 0; kbl < 2; ++kbl)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          xg[kbl][e] = p[(size_t)(16 * kbl + e) * ld + (lane_off + (uint32_t)rw)];
+  for (int item = blockIdx.x; item < nitems; item += G) {
+    const int qi = item / S, sl = item % S;
+    int q = 0;
+    for (int b0 = 0, seen = 0; b0 < nq; b0 += SVDJ_WAVE) {  // the qi-th active quad
+      const bool a = active(b0 + lane);
+      const unsigned long long m = __ballot(a);
+      const int cnt = __popcll(m);
+      if (seen <= qi && qi < seen + cnt) {
+        const int pre = __popcll(m & ((1ull << lane) - 1ull));
+        q = b0 + __ffsll((long long)__ballot(a && pre == qi - seen)) - 1;
+      }
+      seen += cnt;
     }
-    const bf16x8* tp = Tq + (size_t)kc * TCH;
+    q = __builtin_amdgcn_readfirstlane(q);
+    const int t0 = (int)((long long)sl * nt / S), t1 = (int)((long long)(sl + 1) * nt / S);
+    // this wave's split T - I slice: Ts[q][kb][ct = wave][part][lane]
+    bf16x8 qf[16][NP];
+    {
+      const bf16x8* tp = Ts + ((size_t)q * 16 * 8 + wave) * NP * SVDJ_WAVE + lane;
 #pragma unroll
-    for (int j = 0; j < TPT; ++j) tg[j] = tp[j * kQuadApplyThreads + tid];
+      for (int kb = 0; kb < 16; ++kb)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) qf[kb][p] = tp[(kb * 8 * NP + p) * SVDJ_WAVE];
+    }
+    // this wave's 32 columns: block wave >> 1 of [a b c d], half wave & 1
+    const int32_t* qp = pairs + 4 * q;
+    const int qb = wave >> 1;
+    const int col0 = __builtin_amdgcn_readfirstlane(qp[(qb & 1) * 2 + (qb >> 1)] * 64 + (wave & 1) * 32);
+    float* const ownA = A + (size_t)col0 * lda;
+    float* const ownV = V ? V + (size_t)col0 * ldv : nullptr;
+
+    auto dma = [&](int t, int buf) {  // raw tile t, own 32 columns -> R[buf] (4 x 1 KB)
+      const bool isA = t < a_tiles;
+      const float* base = isA ? ownA : ownV;
+      const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
+      char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(base + (size_t)(8 * i + (lane >> 3)) * ld + r0 + (lane & 7) * 4,
+                                         dst + i * 1024, 16, 0, 0);
+    };
+    auto tile = [&](int t, auto bufc) {
+      constexpr int buf = decltype(bufc)::value;
+      // 1. own DMA of tile t landed (younger: stores of t-1, DMA of t+1)
+      const int younger = (t > t0 ? 16 : 0) + (t + 1 < t1 ? 4 : 0);
+      if (younger == 20) wait_vmcnt<20>();
+      else if (younger == 16) wait_vmcnt<16>();
+      else if (younger == 4) wait_vmcnt<4>();
+      else wait_vmcnt<0>();
+      // 2. split own columns into the shared B-fragment image S[buf]
+      {
+        const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
+        bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
+#pragma unroll
+        for (int kbl = 0; kbl < 2; ++kbl) {
+          bf16x8 parts[NP];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            __bf16 pp[NP];
+            split_bf16<NP>(R[(16 * kbl + 8 * h + e) * 32 + c], pp);
+#pragma unroll
+            for (int i = 0; i < NP; ++i) parts[i][e] = pp[i];
+          }
+#pragma unroll
+          for (int i = 0; i < NP; ++i) Sw[((2 * wave + kbl) * NP + i) * SVDJ_WAVE] = parts[i];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // 3. 16 k blocks x (1 + 5) MFMAs against the register-resident slice
+      const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
+      f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
+#pragma unroll
+      for (int kb = 0; kb < 16; ++kb) {
+        bf16x8 xs[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) xs[i] = Sr[(kb * NP + i) * SVDJ_WAVE];
+        lo = mfma_split<NP, 1>(qf[kb], xs, lo);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+      }
+      acc += lo;
+      // 4. own raw values from the image (acc layout: register 4g + i is
+      //    column 8g + 4h + i = k block 2 wave + (g >> 1), lane half g & 1,
+      //    element 4h + i) and the delta-form store, in place
+      {
+        const bool isA = t < a_tiles;
+        float* const own = isA ? ownA : ownV;
+        const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
+        const uint32_t st_off = (uint32_t)(4 * h * ld + c) + (uint32_t)r0;
+        const char* Sb = lds + buf * L::S_BYTES;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int kb = 2 * wave + (g >> 1), ln = c + 32 * (g & 1);
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < NP; ++i) {  // x = (x0 + x1) + x2, exact
+            const uint2 u = *reinterpret_cast<const uint2*>(Sb + ((kb * NP + i) * SVDJ_WAVE + ln) * 16 + 8 * h);
+            const float w0 = __uint_as_float(u.x << 16), w1 = __uint_as_float(u.x & 0xffff0000u);
+            const float w2 = __uint_as_float(u.y << 16), w3 = __uint_as_float(u.y & 0xffff0000u);
+            v[0] = i ? v[0] + w0 : w0;
+            v[1] = i ? v[1] + w1 : w1;
+            v[2] = i ? v[2] + w2 : w2;
+            v[3] = i ? v[3] + w3 : w3;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            at_u32(own + (size_t)Mfma<float>::acc_row_uni(4 * g + i) * ld, st_off) = v[i] + acc[4 * g + i];
+        }
+      }
+      // 5. tile t + 2 into the raw image this wave just consumed
+      if (t + 2 < t1) dma(t + 2, buf);
+    };
+    if (t0 < t1) dma(t0, 0);
+    if (t0 + 1 < t1) dma(t0 + 1, 1);
+    for (int t = t0; t < t1; t += 2) {
+      tile(t, std::integral_constant<int, 0>{});
+      if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
+    }
+    // the next item re-stages both images
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+// The six cross Grams of a quad step, every block read ONCE (round 5).  The
+// round-4 form computed them as 3P independent f32-MFMA slabs, each reading
+// its two blocks: every block of a quad was read three times and the f32
+// MFMAs (1/16 of the bf16 rate) set the pace (722 us per 128-pair quad step
+// vs 2 x 215 us for the two single-step Grams it replaces).  Here
+// one workgroup (8 waves) per (quad, row chunk):
+//   * wave w LDS-DMAs column tile w (32 of the quad's 256 columns, [a b c d]
+//     order) of each 32-row slab two slabs ahead into a wave-private raw
+//     image, and splits it into 3 RNE bf16 parts in the shared A/B fragment
+//     image (lane (c, h): column c, rows 8h .. 8h+7 of a 16-row k step);
+//   * the 24 output tiles (6 products x 2 x 2 tiles of 32 x 32) are dealt 3
+//     per wave; each tile takes the 6 products of order < 3 per k step
+//     (leading product and the small ones in two accumulators), the error of
+//     a product below 2^-26 relative, like the split apply;
+//   * the tiles go straight to the slab layout the consumers read: slab
+//     (pair 2q) = C_ac, (2q+1) = C_bd, then per quad C_ad, C_bc, C_ab, C_cd
+//     (the order quad_update_kernel reads), one W x W slab per row chunk.
+constexpr int kGramQThreads = 512;
+struct GramQLds {
+  static constexpr int S_BYTES = 2 * 8 * 3 * SVDJ_WAVE * 16;  // 2 k steps x 8 col tiles x 3 parts
+  static constexpr int R_BYTES = 8 * 32 * 32 * 4;             // raw 32-row slab, wave w at 4 KB * w
+  static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
+};
+static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
+__global__ __launch_bounds__(kGramQThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
+                 int P, int rows_per_chunk, float* __restrict__ slabs) {
+  constexpr int W = 64, NP = 3;
+  using L = GramQLds;
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  const int q = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 31, h = lane >> 5;
+  const int32_t* qp = pairs + 4 * q;  // (a, c), (b, d)
+  auto blk = [&](int qb) { return qp[(qb & 1) * 2 + (qb >> 1)]; };  // [a b c d] -> block id
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(m_pad, r_begin + rows_per_chunk);
+  const int ns = (r_end - r_begin) / 32;  // rows_per_chunk and m_pad are multiples of 128
+  const float* own = A + (size_t)__builtin_amdgcn_readfirstlane(blk(wave >> 1) * W + (wave & 1) * 32) * lda;
+  // products in [a b c d] block order: (x, y) and the slab each goes to
+  constexpr int PX[6] = {0, 1, 0, 1, 0, 2}, PY[6] = {2, 3, 3, 2, 1, 3};  // ac bd ad bc ab cd
+  auto dma = [&](int sl, int buf) {
+    const int r0 = r_begin + 32 * sl;
+    char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(own + (size_t)(8 * i + (lane >> 3)) * lda + r0 + (lane & 7) * 4,
+                                       dst + i * 1024, 16, 0, 0);
   };
-  auto lstore = [&](int kc, int slot, int buf) {
-    if ((kc >> 2) == chh) {
+  f32x16 acc[3], lo[3];
 #pragma unroll
-      for (int kbl = 0; kbl < 2; ++kbl) {
+  for (int j = 0; j < 3; ++j) acc[j] = lo[j] = Mfma<float>::zero();
+  auto slab = [&](int sl, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    if (sl + 1 < ns) wait_vmcnt<4>();
+    else wait_vmcnt<0>();
+    {  // split column tile `wave` of this slab: rows 16 kk + 8h .. + 7 of column c
+      const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
+      bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(R + c * 32 + 16 * kk + 8 * h);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(R + c * 32 + 16 * kk + 8 * h + 4);
         bf16x8 parts[NP];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          __bf16 p[NP];
-          split_bf16<NP>(xg[kbl][e], p);
+          __bf16 pp[NP];
+          split_bf16<NP>(e < 4 ? v0[e] : v1[e - 4], pp);
 #pragma unroll
-          for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
+          for (int i = 0; i < NP; ++i) parts[i][e] = pp[i];
         }
 #pragma unroll
-        for (int i = 0; i < NP; ++i) Xl[buf][rg][kbl][i][lane] = parts[i];
+        for (int i = 0; i < NP; ++i) Sw[((kk * 8 + wave) * NP + i) * SVDJ_WAVE] = parts[i];
       }
-      // raw values of output tile kc in accumulator layout: register g*4+i
-      // of lane (c, h) is column 8g + 4h + i; lane half h loaded columns
-      // 16 kbl + 8h + e
-      float* xd = xo[slot];
-#pragma unroll
-      for (int kbl = 0; kbl < 2; ++kbl)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float keep = h ? xg[kbl][4 + i] : xg[kbl][i];
-          const float give = h ? xg[kbl][i] : xg[kbl][4 + i];
-          const float got = __int_as_float(half_swap(__float_as_int(give)));
-          xd[(2 * kbl) * 4 + i] = h ? got : keep;
-          xd[(2 * kbl + 1) * 4 + i] = h ? keep : got;
-        }
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
-    for (int j = 0; j < TPT; ++j) Tl[buf][j * kQuadApplyThreads + tid] = tg[j];
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int t = 3 * wave + j, pr = t >> 2, ti = (t >> 1) & 1, tj = t & 1;
+        const int cx = 2 * PX[pr] + ti, cy = 2 * PY[pr] + tj;  // column tiles
+        bf16x8 xf[NP], yf[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          xf[i] = Sr[((kk * 8 + cx) * NP + i) * SVDJ_WAVE];
+          yf[i] = Sr[((kk * 8 + cy) * NP + i) * SVDJ_WAVE];
+        }
+        lo[j] = mfma_split<NP, 1>(xf, yf, lo[j]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf[0], yf[0], acc[j], 0, 0, 0);
+      }
+    if (sl + 2 < ns) dma(sl + 2, buf);
   };
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = Mfma<float>::zero();
-  gload(0);
-  lstore(0, 0, 0);
-  __syncthreads();
-  // chunk kc = 4 kq + ki: ki unrolled so the raw-value slots xo[ki] are
-  // static registers, kq rolled (a fully unrolled loop spilled)
-#pragma unroll 1
-  for (int kq = 0; kq < 2; ++kq) {
-#pragma unroll
-    for (int ki = 0; ki < 4; ++ki) {
-      const int kc = 4 * kq + ki, buf = ki & 1;
-      if (kc + 1 < NKC) gload(kc + 1);
-#pragma unroll
-      for (int kbl = 0; kbl < 2; ++kbl) {
-        bf16x8 xs[NP];
-#pragma unroll
-        for (int i = 0; i < NP; ++i) xs[i] = Xl[buf][rg][kbl][i][lane];
-#pragma unroll
-        for (int ot = 0; ot < 4; ++ot) {
-          const int ct = 4 * chh + ot;
-          bf16x8 qf[NP];
-#pragma unroll
-          for (int i = 0; i < NP; ++i) qf[i] = Tl[buf][((kbl * 8 + ct) * NP + i) * SVDJ_WAVE + lane];
-          // small products first, the leading one last, one accumulator:
-          // a second one for the small terms (apply_split_kernel) does not fit
-          // next to the 4 x 16 raw values (spills); a quad applies T to each
-          // column half as often as two single steps
-          acc[ot] = mfma_split<NP, 1>(qf, xs, acc[ot]);
-          acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[0], xs[0], acc[ot], 0, 0, 0);
-        }
-      }
-      if (kc + 1 < NKC) lstore(kc + 1, (ki + 1) & 3, buf ^ 1);
-      __syncthreads();
-    }
+  if (ns > 0) dma(0, 0);
+  if (ns > 1) dma(1, 1);
+  for (int sl = 0; sl < ns; sl += 2) {
+    slab(sl, std::integral_constant<int, 0>{});
+    if (sl + 1 < ns) slab(sl + 1, std::integral_constant<int, 1>{});
   }
-  // every read of this workgroup's rows is done: store in place
+  // the wave's three tiles straight to their slabs
 #pragma unroll
-  for (int ot = 0; ot < 4; ++ot) {
-    float* p = col_ptr(4 * chh + ot);
+  for (int j = 0; j < 3; ++j) {
+    const int t = 3 * wave + j, pr = t >> 2, ti = (t >> 1) & 1, tj = t & 1;
+    const size_t sidx = pr < 2 ? (size_t)(2 * q + pr) * nchunk + chunk
+                               : (size_t)P * nchunk + ((size_t)q * 4 + (pr - 2)) * nchunk + chunk;
+    float* out = slabs + sidx * (W * W) + (ti * 32) * W + tj * 32 + c;
+    const f32x16 v = acc[j] + lo[j];
 #pragma unroll
-    for (int e = 0; e < 16; ++e)
-      p[(size_t)Mfma<float>::acc_row_uni(e) * ld + (st_off + (uint32_t)rw)] = xo[ot][e] + acc[ot][e];
+    for (int e = 0; e < 16; ++e) out[Mfma<float>::acc_row(e, lane) * W] = v[e];
   }
 }
 
@@ -2203,22 +2365,22 @@ struct Geometry {
   int gchunks, grows;  // gram
   int a_chunks, rows_a, v_chunks, rows_v;
   // quad steps (fp32 W = 64): gram row chunks, apply row chunks
-  int qgch, qgrows, qa_chunks, qv_chunks, qrows;
+  int qgch, qgrows;
 };
 
-// Quad-step geometry: the GRAM_QUAD launch has 3P workgroups per row chunk
-// and each of its slabs is summed by evd_cross_kernel / quad_update_kernel,
-// so it uses few chunks (~512 workgroups); the apply has 2 workgroups per
-// quad and row chunk, one per CU (LDS), ~4096 of them.
+// Quad-step geometry: row chunks of gram_quad_kernel (its slabs are summed
+// by evd_cross_kernel / quad_update_kernel); the apply is a persistent grid.
 static void quad_geometry(Geometry& g, int P, int m_pad, int n_v) {
-  const int want = (512 + 3 * P - 1) / (3 * P);
+  // gram_quad_kernel: one workgroup (160 KB LDS, one per CU) per quad and row
+  // chunk, ~256 of them; from 32 quads per launch every quad keeps 8 chunks,
+  // so a merged one-GPU launch (two chains' quads in one) sums every Gram
+  // exactly as the two chains do (bitwise the same solve, as make_geometry)
+  const int nq = P / 2 > 0 ? P / 2 : 1;
+  const int want = nq >= 32 ? 8 : (256 + nq - 1) / nq;
   const int maxc = m_pad / 128;
   g.qgch = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.qgrows = round_up((m_pad + g.qgch - 1) / g.qgch, 128);
   g.qgch = (m_pad + g.qgrows - 1) / g.qgrows;
-  g.qrows = kQuadRows;
-  g.qa_chunks = (m_pad + kQuadRows - 1) / kQuadRows;
-  g.qv_chunks = n_v > 0 ? (n_v + kQuadRows - 1) / kQuadRows : 0;
 }
 
 static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
@@ -2269,21 +2431,27 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
 }
 
 static size_t rup256(size_t b) { return (b + 255) / 256 * 256; }
-// Quad-step scratch (fp32 W = 64 only): GRAM_QUAD slabs (3P pairs), T1
-// (fp64 Q of the P step-s pairs), the step-(s+1) couplings, T (P/2 quads x
-// 256 x 256 fp32), and double-buffered split T (3 parts) and skip flags of
-// both EVDs.
+// Quad-step scratch (fp32 W = 64, only when the step list has quad steps):
+// the 3P Gram slabs, T1 (fp64 Q of the P step-s pairs), the step-(s+1)
+// couplings, T (P/2 quads x 256 x 256 fp32), double-buffered split T (3 bf16
+// parts = 1.5 x T each) and the skip flags of both EVDs (chain_init's layout).
 static bool has_quad(int esize, int W) { return esize == 4 && W == 64; }
 static size_t quad_bytes(int P, int m_pad) {
   Geometry g;
   quad_geometry(g, P, m_pad, 0);
   constexpr int W = 64;
-  const size_t sk = rup256((size_t)P * sizeof(int32_t));
+  const size_t kstride = rup256((size_t)P * sizeof(int32_t));
+  const size_t tstride = rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float));
   return rup256((size_t)3 * P * g.qgch * W * W * sizeof(float)) +
          rup256((size_t)P * 4 * W * W * sizeof(double)) + rup256((size_t)P * W * W * sizeof(float)) +
-         3 * rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float)) * 2 + 4 * sk;
+         4 * tstride + 4 * kstride;
 }
-static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
+static bool has_quad_steps(const int32_t* modes, int steps) {
+  for (int s = 0; modes && s < steps; ++s)
+    if (modes[s] == 4) return true;
+  return false;
+}
+static size_t ws_bytes_for(int esize, int W, int P, int m_pad, bool quad) {
   Geometry g = make_geometry(W, P, m_pad, 0);
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
@@ -2293,7 +2461,7 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad) {
   // reads) + the cross EVD's rotation records and step counts (consumed by
   // qbuild(s) before evd(s+1) on the same stream: single-buffered)
   return rup256(slabs) + 2 * rup256(q) + 2 * rup256(sk) + rup256(rec) + rup256(sk) +
-         (has_quad(esize, W) ? quad_bytes(P, m_pad) : 0);
+         (quad && has_quad(esize, W) ? quad_bytes(P, m_pad) : 0);
 }
 
 // One chain of steps: resident buffers, its pair list and its workspace.
@@ -2324,7 +2492,12 @@ template <typename T, int W>
 static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int ldv, T* D,
                       const int32_t* pairs, int P, int steps, const int32_t* modes, void* ws,
                       size_t ws_bytes, int mma, hipStream_t st) {
-  const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad);
+  const bool quad = has_quad_steps(modes, steps);
+  if (quad && !has_quad(sizeof(T), W)) {
+    set_error("quad steps need fp32 data and W = 64");
+    return -3;
+  }
+  const size_t need = ws_bytes_for(sizeof(T), W, P, m_pad, quad);
   if (ws_bytes < need) {
     set_error("workspace too small: %zu < %zu", ws_bytes, need);
     return -4;
@@ -2361,7 +2534,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   c.Tq = nullptr;
   c.Ts[0] = c.Ts[1] = nullptr;
   c.skip1[0] = c.skip1[1] = c.skip2[0] = c.skip2[1] = nullptr;
-  if (has_quad(sizeof(T), W)) {
+  if (quad) {
     c.qslabs = (float*)w;
     w += rup256((size_t)3 * P * c.g.qgch * W * W * sizeof(float));
     c.T1 = (double*)w;
@@ -2395,8 +2568,8 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     const int b = s & 1;
     const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
     const int32_t* pr1 = pr + 2 * c.P;
-    hipLaunchKernelGGL((gram_cross_f32_kernel<GRAM_QUAD>), dim3(3 * c.P, c.g.qgch, 1),
-                       dim3(kGramThreads), 0, c.st, c.A, c.lda, c.m_pad, pr, c.g.qgrows, c.qslabs, 0);
+    hipLaunchKernelGGL(gram_quad_kernel, dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0, c.st,
+                       c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
                        pr, c.qslabs, c.g.qgch, c.D, c.rec, c.nsteps, c.skip1[b], (float)tol,
@@ -2516,17 +2689,16 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
         set_error("quad steps run the split-bf16 apply (mma 1 or 2), got %d", mma);
         return -3;
       }
-      const int nq = c.P / 2, qv = c.V ? c.g.qv_chunks : 0;
-      const int tpq = c.g.qa_chunks + qv;
-      const dim3 grid(nq * tpq);
+      // T-stationary persistent apply (apply_quad_ts_kernel)
+      const int nq = c.P / 2, at = c.m_pad / 32, vt = c.V ? c.n_v / 32 : 0;
       if (mma == 1)
-        hipLaunchKernelGGL((apply_quad_kernel<3>), grid, dim3(kQuadApplyThreads), 0, c.st, c.A,
-                           c.lda, c.g.qa_chunks, c.V, c.ldv, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b], tpq);
+        hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
+                           c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
+                           c.skip2[b]);
       else
-        hipLaunchKernelGGL((apply_quad_kernel<2>), grid, dim3(kQuadApplyThreads), 0, c.st, c.A,
-                           c.lda, c.g.qa_chunks, c.V, c.ldv, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b], tpq);
+        hipLaunchKernelGGL((apply_quad_ts_kernel<2>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
+                           c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
+                           c.skip2[b]);
       SVDJ_LAUNCH_CHECK();
       return 0;
     } else {
@@ -2674,8 +2846,8 @@ extern "C" int svdj_choose_inner_order(int dtype, int W, int pairs) {
 // rank plan, W = 32: 8.55 vs 9.61 ms per sweep with the split).
 extern "C" int svdj_choose_mma(int dtype, int W) { return (dtype == 0 && W == 64) ? 1 : 0; }
 
-extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad) {
-  return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad);
+extern "C" size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad, int quad) {
+  return ws_bytes_for(dtype == 1 ? 8 : 4, W, P, m_pad, quad != 0);
 }
 
 static int check_dims(int m_pad, int lda, const void* V, int n_v, int ldv, int mma) {
@@ -2766,8 +2938,8 @@ extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
                                 int ldv, void* D, int ncols, double tol, int tol_mode,
                                 int max_inner, int max_sweeps, int inner_order, void* ws,
-                                size_t ws_bytes,
-                                uint32_t* metric, double* hist, int mma, void* stream) {
+                                size_t ws_bytes, uint32_t* metric, double* hist, int mma,
+                                int stop_rule, void* stream) {
   if (W <= 0 || ncols % W) {
     set_error("ncols %d not a multiple of W %d", ncols, W);
     return -2;
@@ -2802,11 +2974,11 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
   SVDJ_HIP_CHECK(hipMemcpyAsync(dpairs, h.data(), h.size() * sizeof(int32_t),
                                 hipMemcpyHostToDevice, st));
   int sweeps = 0, rc = 0;
-  uint32_t hm[2];
+  uint32_t hm[6];
   // underflow floor of this solve (metric[2..3])
   rc = svdj_set_norm_floor_scaled(dtype, m_pad, D, ncols, metric, stream);
   for (int sw = 0; sw < max_sweeps && rc >= 0; ++sw) {
-    if (hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st) != hipSuccess) { rc = -100; break; }
+    if (svdj_reset_metric(metric, stream) != 0) { rc = -100; break; }
     rc = svdj_block_steps(dtype, W, m_pad, A, lda, V, n_v, ldv, D, dpairs, P, steps,
                           modes.data(), tol, tol_mode, max_inner, ws, ws_bytes, metric, mma,
                           stream);
@@ -2817,11 +2989,12 @@ extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, v
       rc = -100;
       break;
     }
-    float mx;
+    float mx, ms;
     memcpy(&mx, &hm[0], sizeof(float));
+    memcpy(&ms, &hm[4], sizeof(float));
     if (hist) hist[sw] = mx;
     sweeps = sw + 1;
-    if (hm[1] == 0) break;
+    if (svdj_sweep_converged_inline(mx, ms, hm[1], hm[5], tol, tol_mode, stop_rule)) break;
   }
   (void)hipFreeAsync(dpairs, st);
   return rc ? rc : sweeps;
@@ -2856,6 +3029,29 @@ extern "C" int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_p
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("svdj_gram_cross launch: %s", hipGetErrorString(e));
+    return -101;
+  }
+  return 0;
+}
+
+// The six cross Grams of a quad step (fp32, W = 64) alone (tests / kernel
+// A/B): pairs = the step's P pairs in quad order ((a,c),(b,d) per quad);
+// slabs (3P x nchunk x W x W): [0, P) the pairs' Grams, then C_ad, C_bc, C_ab,
+// C_cd of every quad (gram_quad_kernel).
+extern "C" int svdj_gram_quad(const void* A, int lda, int m_pad, const int32_t* pairs, int P,
+                              int rows_per_chunk, void* slabs, void* stream) {
+  if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad || lda % 4 || P <= 0 || P % 2 ||
+      rows_per_chunk <= 0 || rows_per_chunk % SVDJ_ROW_ALIGN) {
+    set_error("svdj_gram_quad: bad m_pad/lda/P/rows %d/%d/%d/%d", m_pad, lda, P, rows_per_chunk);
+    return -2;
+  }
+  const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
+  hipLaunchKernelGGL(gram_quad_kernel, dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
+                     (hipStream_t)stream, (const float*)A, lda, m_pad, pairs, P, rows_per_chunk,
+                     (float*)slabs);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("svdj_gram_quad launch: %s", hipGetErrorString(e));
     return -101;
   }
   return 0;

@@ -158,6 +158,14 @@ extern "C" int svdj_set_norm_floor(double floor, uint32_t* metric, void* stream)
   return 0;
 }
 
+// Per-sweep words of a block-path metric: [0], [1] and [4..7] (svdj_stop.h).
+extern "C" int svdj_reset_metric(uint32_t* metric, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  SVDJ_HIP_CHECK(hipMemsetAsync(metric, 0, 2 * sizeof(uint32_t), st));
+  SVDJ_HIP_CHECK(hipMemsetAsync(metric + 4, 0, (SVDJ_METRIC_WORDS - 4) * sizeof(uint32_t), st));
+  return 0;
+}
+
 // Scale-relative floor (ops/kernels.py norm_floor): metric[2..3] =
 // max(m realmin, m realmin / eps * max_j D[j]) over the n squared norms D,
 // on the device (one workgroup).

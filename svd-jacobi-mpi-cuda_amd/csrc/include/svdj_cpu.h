@@ -90,6 +90,15 @@ double svdj_cpu_residual_f64(int m, int n, int k, const double* A, int lda,
 // ||Q^T Q - I||_F for column-major Q (m x k).
 double svdj_cpu_orth_f64(int m, int k, const double* Q, int ldq, int num_threads);
 
+// ------------------------------------------------------------------ stop test
+// Block-path sweep stop test (svdj_stop.h): 0 = continue, 1 = the sweep
+// rotated nothing, 2 = the second-order rule (relative mode,
+// second_order != 0).  mx, ms, nrot_pairs, nrot_cols: the sweep's global
+// largest coupling, largest effective sine of an applied rotation, rotated
+// block pairs and applied column rotations.
+int svdj_sweep_converged(double mx, double ms, double nrot_pairs, double nrot_cols, double tol,
+                         int tol_mode, int second_order);
+
 const char* svdj_cpu_version(void);
 
 #ifdef __cplusplus

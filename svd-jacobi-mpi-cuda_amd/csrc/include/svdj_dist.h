@@ -93,6 +93,9 @@ typedef struct {
   int progress;               // 1: rank 0 prints one line per sweep on stderr
   int inner_order_used;       // out: the resolved EVD order (0 cyclic, 1 bipartite, 2 cross)
   int exchange_used;          // out: the resolved exchange (1 direct, 2 spread)
+  int stop_rule;              // 1: a sweep also ends the iteration by the second-order rule
+                              // (svdj_stop.h; relative mode); 0: only a sweep without
+                              // rotations does.  converged (out) = 1 (no rotation) or 2
 } svdj_dist_problem;
 
 // Persistent per-rank state for repeated solves of one geometry: workspaces,

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #define SVDJ_ROW_ALIGN 128
+#include "svdj_stop.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -61,17 +62,19 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //   modes   host   int32 [steps] (0 cross / 1 full / 2 cross with the bipartite
 //           EVD ordering, W steps instead of 2W-1 / 3 cross with the
 //           cross-only bipartite EVD), NULL = all cross
-//   metric  device uint32[4]: [0] max convergence value (float bits), [1]
-//           rotated pairs, [2..3] the underflow floor (double,
-//           svdj_set_norm_floor; 0 = off).
+//   metric  device uint32[SVDJ_METRIC_WORDS] (svdj_stop.h): [0] max
+//           convergence value (float bits), [1] rotated pairs, [2..3] the
+//           underflow floor (double, svdj_set_norm_floor; 0 = off), [4] the
+//           largest |sin| of an applied rotation (float bits).
 //   tol_mode 0: rotate when |g_pq| > tol sqrt(g_pp g_qq) (relative, default);
 //            1: when |g_pq| > tol (the reference's absolute TOLERANCE test).
 //   mma     matrix-core mode: 0 native (f32 / f64 MFMA), 1 fp32 data on bf16
 //           MFMA with a 3-way bf16 split (6 products, fp32-level accuracy),
 //           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
 //           Both split modes apply Y = X + X (Q - I), the identity in fp32.
-// Workspace size for one step: svdj_block_workspace_bytes().
-size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad);
+// Workspace size for steps of P pairs: svdj_block_workspace_bytes(); quad != 0
+// when the step list holds quad steps (modes 4/5: fp32, W = 64).
+size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad, int quad);
 // inner_order code (1 bipartite, 2 cross-only) for steps of `pairs` pairs of
 // W-wide blocks of data type `dtype` (0 fp32, 1 fp64): models/block.py
 // choose_inner_order.
@@ -101,17 +104,27 @@ int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
 // step, 1 = bipartite EVD in the cross steps (mode 2), 2 = cross-only
-// bipartite EVD (mode 3).  Returns sweeps, <0 on error.
+// bipartite EVD (mode 3).  stop_rule 1: a sweep also ends the iteration by
+// the second-order rule of svdj_stop.h (relative mode), 0: only a sweep
+// without rotations does.  Returns sweeps, <0 on error.
 int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int n_v, int ldv, void* D, int ncols, double tol, int tol_mode,
                      int max_inner_sweeps, int max_sweeps, int inner_order, void* workspace,
                      size_t ws_bytes, uint32_t* metric, double* hist,
-                     int mma, void* stream);
+                     int mma, int stop_rule, void* stream);
+// Zero the per-sweep words of a block-path metric ([0], [1], [4..7]); the
+// floor ([2..3]) stays.
+int svdj_reset_metric(uint32_t* metric, void* stream);
 
 // Diagnostic hooks.  Cross Gram slabs (P x nchunk x W x W) of A_bi^T A_bj
 // for a device pair list with the given row chunking (fp32).
 int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_pad,
                     const int32_t* pairs, int P, int rows_per_chunk, void* slabs, void* stream);
+// The six cross Grams of a quad step (fp32, W = 64; pairs in quad order,
+// P even): slabs (3P x nchunk x W x W) = the P pairs' Grams, then C_ad, C_bc,
+// C_ab, C_cd of every quad.
+int svdj_gram_quad(const void* A, int lda, int m_pad, const int32_t* pairs, int P,
+                   int rows_per_chunk, void* slabs, void* stream);
 // X <- X Q for one pair of column blocks (X = 2W columns, leading dimension
 // ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major 2W x 2W on the
 // device, with matrix-core mode `mma` (as svdj_block_steps).

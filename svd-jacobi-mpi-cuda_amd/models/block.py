@@ -85,12 +85,20 @@ def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
 
 
 def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
-    """Quad steps for config quad="auto": off.  Measured on MI355X, 16384^2
-    fp32 1 GPU (profiles/r4_quad): the fused K = 256 apply reads T (384 KB
-    split per quad) from L2/MALL for every 128-row tile and ran at 1.71 ms
-    per quad step vs 2 x 0.70 ms for the two W = 64 applies it replaces;
-    whole solve 5.38 s vs 4.87 s.  Selectable with quad="on"."""
-    return False
+    """Quad steps for config quad="auto": on ONE GPU when a chain step holds
+    >= 64 pairs (k // 2 >= 64, 16384^2 and up; the merged one-GPU issue
+    then runs 128-pair quad steps), off otherwise.
+
+    Measured on MI355X (profiles/r5_quad), with the round-5 kernels: the six
+    cross Grams read each block once on split-bf16 MFMAs (gram_quad_kernel)
+    and the K = 256 apply keeps T register-resident in a persistent grid
+    (apply_quad_ts_kernel).  16384^2 fp32: 3.69 s vs 4.72 s per solve (18
+    sweeps both; residual 1.07e-5 vs 1.37e-5, orth U/V max 1.53e-5 /
+    7.2e-6 vs 1.53e-5 / 9.3e-6); 128-pair step probe 879 vs 1203 us per
+    step.  With few quads per step the per-workgroup T load and the EVD
+    chain latency dominate: 8192^2 821 vs 678 ms, 4096^2 358 vs 132 ms,
+    16384^2 rank plans P=2/4/8 170/146/192 vs 163/84/53 ms per sweep."""
+    return P == 1 and k // 2 >= 64 and quad_supported(dtype, W, mma, k)
 
 
 def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
@@ -137,7 +145,7 @@ class BlockJacobi(Solver):
             inner = resolve_inner_order(cfg.inner_order, W, ncols // (2 * W), dtype)
             sweeps, hist = K.block_solve(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps,
                                          cfg.max_sweeps, mma=mma, tol_mode=cfg.tol_mode,
-                                         inner_order=inner)
+                                         inner_order=inner, stop_rule=cfg.stop_rule)
             S = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         U = At[:n, :m].t() if jobu != SVDOptions.NoVec else None
         V = Vt[:n, :n].t() if want_v else None

@@ -78,6 +78,8 @@ def cpu_lib():
         _sig(lib, "svdj_cpu_residual_f64", c_double,
              [c_int, c_int, c_int, c_f64_p, c_int, c_f64_p, c_int, c_f64_p, c_f64_p, c_int, c_int])
         _sig(lib, "svdj_cpu_orth_f64", c_double, [c_int, c_int, c_f64_p, c_int, c_int])
+        _sig(lib, "svdj_sweep_converged", c_int,
+             [c_double, c_double, c_double, c_double, c_double, c_int, c_int])
         _sig(lib, "svdj_cpu_version", C.c_char_p, [])
         _cpu = lib
         return lib
@@ -107,7 +109,7 @@ def hip_lib():
         _sig(lib, "svdj_scalar_solve", c_int,
              [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
               c_double, c_int, c_int, c_void_p, c_f64_p, c_void_p])
-        _sig(lib, "svdj_block_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int])
+        _sig(lib, "svdj_block_workspace_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int])
         _sig(lib, "svdj_choose_inner_order", c_int, [c_int, c_int, c_int])
         _sig(lib, "svdj_block_steps", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
@@ -120,9 +122,12 @@ def hip_lib():
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
-              c_void_p])
+              c_int, c_void_p])
+        _sig(lib, "svdj_reset_metric", c_int, [c_void_p, c_void_p])
         _sig(lib, "svdj_gram_cross", c_int,
              [c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
+        _sig(lib, "svdj_gram_quad", c_int,
+             [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_apply_q", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,
@@ -148,7 +153,8 @@ class DistProblem(C.Structure):
                 ("handle", c_void_p), ("hist", c_f64_p), ("sweeps", c_int),
                 ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double),
                 ("exchanges", C.c_longlong), ("bytes_sent", C.c_longlong),
-                ("progress", c_int), ("inner_order_used", c_int), ("exchange_used", c_int)]
+                ("progress", c_int), ("inner_order_used", c_int), ("exchange_used", c_int),
+                ("stop_rule", c_int)]
 
 
 def dist_lib_path() -> Path:

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import reference as ref
-from ._native import NativeError, hip_check, hip_lib
+from ._native import NativeError, cpu_lib, hip_check, hip_lib
 
 ROW_ALIGN = 128
 SUPPORTED_BLOCK = {torch.float32: (32, 64), torch.float64: (32, 64)}
@@ -77,17 +77,28 @@ def _check_layout(At: torch.Tensor, m_pad: int):
 
 
 # ------------------------------------------------------------------ metric
+METRIC_WORDS = 8  # csrc/include/svdj_stop.h SVDJ_METRIC_WORDS
+
+
 def new_metric(device) -> torch.Tensor:
     """Per-sweep stop-test state: [0] max convergence value, [1] rotated
-    pairs, and (block path) the negligible-column floor of the solve
-    (device: int32[4], the floor a double in [2..3]; CPU: float64[3])."""
+    pairs, the negligible-column floor of the solve (block path), and for the
+    block path's second-order stop test the largest effective sine of an
+    applied rotation and the number of column rotations applied.  Device:
+    int32[8] (csrc/include/svdj_stop.h: floor a double in [2..3], sine float
+    bits in [4], count [5]); CPU: float64[5] (floor [2], sine [3], count [4])."""
     if torch.device(device).type == "cpu":
-        return torch.zeros(3, dtype=torch.float64)
-    return torch.zeros(4, dtype=torch.int32, device=device)
+        return torch.zeros(5, dtype=torch.float64)
+    return torch.zeros(METRIC_WORDS, dtype=torch.int32, device=device)
 
 
 def reset_metric(metric: torch.Tensor):
-    metric[:2].zero_()  # the floor (set once per solve) stays
+    """Zero the per-sweep words; the floor (set once per solve) stays."""
+    metric[:2].zero_()
+    if metric.device.type == "cpu":
+        metric[3:].zero_()
+    else:
+        metric[4:].zero_()
 
 
 def norm_floor(dtype: torch.dtype, m: int, dmax: float = 1.0) -> float:
@@ -123,8 +134,41 @@ def read_metric(metric: torch.Tensor):
 def metric_as_float_pair(metric: torch.Tensor) -> torch.Tensor:
     """Device-side (maxconv, rotations) as float64 without host sync."""
     if metric.device.type == "cpu":
-        return metric.clone()
+        return metric[:2].clone()
     return torch.stack([metric[0:1].view(torch.float32).double()[0], metric[1].double()])
+
+
+def metric_stop_values(metric: torch.Tensor) -> torch.Tensor:
+    """(maxconv, max effective sine, rotated pairs, column rotations) as
+    float64, device-side for device metrics (no host sync)."""
+    if metric.device.type == "cpu":
+        return torch.stack([metric[0], metric[3], metric[1], metric[4]]).clone()
+    f = metric.view(torch.float32)
+    u = metric[5:6].view(torch.int32)[0].double()
+    u = torch.where(u < 0, u + 2.0 ** 32, u)  # uint32 count
+    return torch.stack([f[0].double(), f[4].double(), metric[1].double(), u])
+
+
+def read_stop(metric: torch.Tensor):
+    """(max convergence value, max effective sine, rotated pairs, column
+    rotations) -- synchronises."""
+    v = metric_stop_values(metric).cpu()
+    return float(v[0]), float(v[1]), int(v[2]), int(v[3])
+
+
+STOP_RULES = {"no_rotation": 0, "second_order": 1}
+
+
+def sweep_converged(mx: float, ms: float, nrot_pairs: float, nrot_cols: float, tol: float,
+                    tol_mode="relative", stop_rule="second_order") -> int:
+    """The block path's sweep stop test (csrc/include/svdj_stop.h, the same
+    native code every engine runs): 0 continue, 1 the sweep rotated nothing,
+    2 its rotations were all noise-level (second-order rule:
+    nrot_cols * mx * ms <= tol / 2)."""
+    rule = STOP_RULES[stop_rule] if isinstance(stop_rule, str) else int(stop_rule)
+    return int(cpu_lib().svdj_sweep_converged(float(mx), float(ms), float(nrot_pairs),
+                                              float(nrot_cols), float(tol),
+                                              tol_mode_code(tol_mode), rule))
 
 
 # --------------------------------------------------------------- utilities
@@ -222,15 +266,16 @@ def scalar_solve(At, Vt, m_pad, sched, tol, tol_mode, max_sweeps):
 _WS_CACHE: dict = {}
 
 
-def block_workspace(dtype, W, P, m_pad, device, slot: int = 0, pool: dict | None = None
-                    ) -> torch.Tensor:
-    """Per (device, shape, slot) workspace; concurrent chains use distinct
-    slots.  ``pool`` is the caller's own cache (a solver instance owns one, so
-    solvers running concurrently -- e.g. several ranks in one process -- never
-    share scratch); None uses the module-wide cache."""
-    nbytes = int(hip_lib().svdj_block_workspace_bytes(dtype_code(dtype), W, P, m_pad))
+def block_workspace(dtype, W, P, m_pad, device, slot: int = 0, pool: dict | None = None,
+                    quad: bool = False) -> torch.Tensor:
+    """Per (device, shape, slot, quad) workspace; concurrent chains use
+    distinct slots.  ``pool`` is the caller's own cache (a solver instance owns
+    one, so solvers running concurrently -- e.g. several ranks in one process
+    -- never share scratch); None uses the module-wide cache.  ``quad``: the
+    step list holds quad steps (their scratch is sized only then)."""
+    nbytes = int(hip_lib().svdj_block_workspace_bytes(dtype_code(dtype), W, P, m_pad, int(quad)))
     cache = _WS_CACHE if pool is None else pool
-    key = (torch.device(device), dtype, W, P, m_pad, slot)
+    key = (torch.device(device), dtype, W, P, m_pad, slot, bool(quad))
     ws = cache.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -273,7 +318,8 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
     if steps == 0 or P == 0:
         return
     if At.is_cuda:
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, ws_slot, pool)
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, ws_slot, pool,
+                             quad=any(int(x) == 4 for x in modes))
         md = (C.c_int32 * steps)(*[int(x) for x in modes])
         n_v = Vt.shape[1] if Vt is not None else 0
         ldv = Vt.stride(0) if Vt is not None else 0
@@ -286,19 +332,24 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
         for s in range(steps):
             if modes[s] == 5:  # second step of a quad: done with its first
                 continue
+            stats = {"smax": 0.0}
             if modes[s] == 4:
                 mx, nrot = ref.quad_step(At[:, :m_pad], Vt, D, pairs[s], pairs[s + 1], W, tol,
                                          max_inner, tol_mode=tol_mode_code(tol_mode),
-                                         floor=float(metric[2]) if metric.numel() > 2 else 0.0)
-                metric[0] = max(float(metric[0]), mx)
-                metric[1] += nrot
-                continue
-            mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
-                                      max_inner, tol_mode=tol_mode_code(tol_mode),
-                                      floor=float(metric[2]) if metric.numel() > 2 else 0.0,
-                                      order={2: "bipartite", 3: "cross"}.get(modes[s], "cyclic"))
+                                         floor=float(metric[2]) if metric.numel() > 2 else 0.0,
+                                         stats=stats)
+            else:
+                mx, nrot = ref.block_step(At[:, :m_pad], Vt, D, pairs[s], W, modes[s] == 1, tol,
+                                          max_inner, tol_mode=tol_mode_code(tol_mode),
+                                          floor=float(metric[2]) if metric.numel() > 2 else 0.0,
+                                          order={2: "bipartite", 3: "cross"}.get(modes[s],
+                                                                                 "cyclic"),
+                                          stats=stats)
             metric[0] = max(float(metric[0]), mx)
             metric[1] += nrot
+            if metric.numel() > 4:
+                metric[3] = max(float(metric[3]), stats["smax"])
+                metric[4] += stats.get("ncols", 0)
 
 
 def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native",
@@ -318,8 +369,10 @@ def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, 
     args = []
     for pairs, modes, slot, stream in (chain_a, chain_b):
         steps, P = int(pairs.shape[0]), int(pairs.shape[1])
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool)
-        md = (C.c_int32 * max(steps, 1))(*step_modes(modes, inner_order))
+        kmodes = step_modes(modes, inner_order)
+        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool,
+                             quad=any(int(x) == 4 for x in kmodes))
+        md = (C.c_int32 * max(steps, 1))(*kmodes)
         args.append((_ptr(pairs), P, steps, md, _ptr(ws), ws.numel(),
                      C.c_void_p(stream.cuda_stream)))
     n_v = Vt.shape[1] if Vt is not None else 0
@@ -346,6 +399,24 @@ def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
     return slabs
 
 
+def gram_quad(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
+              rows_per_chunk: int) -> torch.Tensor:
+    """The six cross Grams of a quad step (fp32, W = 64): ``pairs`` (P, 2) on
+    the device in quad order ((a, c), (b, d) per quad).  Returns the slabs
+    (3P, nchunk, W, W): the P pairs' Grams, then C_ad, C_bc, C_ab, C_cd of
+    every quad (csrc/hip/block.hip gram_quad_kernel)."""
+    _check_layout(At, m_pad)
+    if At.dtype != torch.float32 or W != 64:
+        raise ValueError("gram_quad: fp32 data, W = 64")
+    pairs = pairs.to(torch.int32).contiguous().to(At.device)
+    P = pairs.shape[0]
+    nchunk = -(-m_pad // rows_per_chunk)
+    slabs = torch.empty(3 * P, nchunk, W, W, dtype=At.dtype, device=At.device)
+    hip_check(hip_lib().svdj_gram_quad(_ptr(At), At.stride(0), m_pad, _ptr(pairs), P,
+                                       rows_per_chunk, _ptr(slabs), _stream(At)), "gram_quad")
+    return slabs
+
+
 def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
     """Xt (2W, ld) rows = columns of X, in place X <- X Q (device tensors)."""
     _check_layout(Xt, Xt.shape[1] // ROW_ALIGN * ROW_ALIGN)
@@ -357,10 +428,10 @@ def apply_q(Xt: torch.Tensor, Q: torch.Tensor, W: int, mma="native"):
 
 
 def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
-                tol_mode="relative", inner_order="cyclic"):
+                tol_mode="relative", inner_order="cyclic", stop_rule="second_order"):
     """Single-device block Jacobi (round-robin over ncols/W blocks, first
-    step of each sweep full; cross steps with ``inner_order``).  Returns
-    (sweeps, hist)."""
+    step of each sweep full; cross steps with ``inner_order``; stop test
+    :func:`sweep_converged`).  Returns (sweeps, hist)."""
     step_modes([], inner_order)  # validates
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
@@ -376,7 +447,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
             ncols, float(tol), tol_mode_code(tol_mode), int(max_inner), int(max_sweeps),
             INNER_ORDERS.index(inner_order), _ptr(ws), ws.numel(), _ptr(metric), hist,
-            mma_code(mma, At.dtype), _stream(At)),
+            mma_code(mma, At.dtype), STOP_RULES[stop_rule], _stream(At)),
             "block_solve")
         return sweeps, [hist[i] for i in range(sweeps)]
     from ..parallel.schedule import round_robin
@@ -391,17 +462,18 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
         reset_metric(metric)
         block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric,
                     tol_mode=tol_mode, inner_order=inner_order)
-        mx, nrot = read_metric(metric)
+        mx, ms, nrot, ncr = read_stop(metric)
         hist.append(mx)
-        if nrot == 0:
+        if sweep_converged(mx, ms, nrot, ncr, tol, tol_mode, stop_rule):
             break
     return len(hist), hist
 
 
 __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric", "set_norm_floor",
+    "METRIC_WORDS", "read_stop", "metric_stop_values", "sweep_converged", "STOP_RULES",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",
-    "gram_cross",
+    "gram_cross", "gram_quad",
 ]

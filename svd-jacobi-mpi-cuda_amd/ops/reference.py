@@ -84,14 +84,19 @@ def bipartite_pairs(W):
     return [[(a, W + (a + t) % W) for a in range(W)] for t in range(W)]
 
 
-def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic", floor: float = 0.0):
+def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic", floor: float = 0.0,
+               stats: dict | None = None):
     """Cyclic parallel Jacobi EVD of a batch of SPD matrices G (P, N, N).
 
     Same orderings (``cyclic``: circle-method round robin over all pairs;
     ``bipartite``: the cross pairs only; ``cross``: the bipartite steps with
     the within-block couplings held at zero, i.e. only the cross couplings
     and the diagonal tracked -- block.hip evd_cross_kernel), threshold and
-    update formulas as the kernels.  Returns (G_diag_final, Q, rotated).
+    update formulas as the kernels.  Returns (G_diag_final, Q, rotated);
+    with ``stats`` (a dict) the second-order stop test's inputs
+    (csrc/include/svdj_stop.h) accumulate: ``smax`` the largest effective
+    sine (|s| times the larger norm ratio after the rotation) and ``ncols``
+    the number of column rotations applied.
     """
     G = G.clone()
     P, N, _ = G.shape
@@ -126,6 +131,14 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic", flo
             c = torch.where(rot, c, torch.ones_like(c))
             s = torch.where(rot, s, torch.zeros_like(s))
             t = torch.where(rot, t, torch.zeros_like(t))
+            if stats is not None:  # second-order stop test (csrc/include/svdj_stop.h)
+                dp, dq = (gpp - t * gpq).abs(), (gqq + t * gpq).abs()
+                lo, hi = torch.minimum(dp, dq), torch.maximum(dp, dq)
+                eff = torch.where(lo > 0, s.abs() * (hi / torch.where(lo > 0, lo, torch.ones_like(lo))).sqrt(),
+                                  torch.ones_like(lo))
+                eff = torch.where(rot, eff, torch.zeros_like(eff))
+                stats["smax"] = max(stats.get("smax", 0.0), float(eff.max()))
+                stats["ncols"] = stats.get("ncols", 0) + int(rot.sum())
             Gp, Gq = G[:, p, :].clone(), G[:, q, :].clone()
             G[:, p, :] = c[:, :, None] * Gp - s[:, :, None] * Gq
             G[:, q, :] = s[:, :, None] * Gp + c[:, :, None] * Gq
@@ -149,7 +162,7 @@ def jacobi_evd(G, tol, max_sweeps, tol_mode: int = 0, order: str = "cyclic", flo
 
 
 def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
-               order: str = "cyclic", floor: float = 0.0):
+               order: str = "cyclic", floor: float = 0.0, stats: dict | None = None):
     """One block step on P disjoint block pairs (pairs: (P, 2) block ids).
 
     Mirrors csrc/hip/block.hip (gram -> evd -> apply).  Updates At, Vt, D in
@@ -185,7 +198,7 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
         R = torch.where(big[:, :, None] & big[:, None, :], R, torch.zeros_like(R))
     maxconv = float(R[:, mask].max()) if mask.any() else 0.0
     lam, Q, rotated = jacobi_evd(G, tol, max_inner, tol_mode,
-                                 order="cyclic" if full else order, floor=floor)
+                                 order="cyclic" if full else order, floor=floor, stats=stats)
     if bool(rotated.any()):
         sel = rotated
         Qs = Q[sel]
@@ -200,7 +213,7 @@ def block_step(At, Vt, D, pairs, W, full, tol, max_inner, tol_mode: int = 0,
 
 
 def quad_step(At, Vt, D, pairs0, pairs1, W, tol, max_inner, tol_mode: int = 0,
-              floor: float = 0.0):
+              floor: float = 0.0, stats: dict | None = None):
     """Two cross steps fused as one quad step (csrc/hip/block.hip "quad
     step"), on the quads of ``pairs0`` ((a,c), (b,d) per quad) and
     ``pairs1`` ((a,d), (b,c)).  The couplings of the second step come from
@@ -238,7 +251,8 @@ def quad_step(At, Vt, D, pairs0, pairs1, W, tol, max_inner, tol_mode: int = 0,
             big = torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1) > floor
             R = torch.where(big[:, :W, None] & big[:, None, W:], R, torch.zeros_like(R))
         mx = float(R.max()) if R.numel() else 0.0
-        lam, Qm, rot = jacobi_evd(Gp, tol, max_inner, tol_mode, order="cross", floor=floor)
+        lam, Qm, rot = jacobi_evd(Gp, tol, max_inner, tol_mode, order="cross", floor=floor,
+                                  stats=stats)
         lam = torch.where(rot[:, None], lam, torch.cat([Dq[:, x_idx], Dq[:, y_idx]], 1))
         Dq[:, x_idx], Dq[:, y_idx] = lam[:, :W], lam[:, W:]
         eye = torch.eye(N, dtype=At.dtype).expand_as(Qm)

@@ -186,6 +186,20 @@ class Communicator:
         h = t.cpu()
         return float(h[0]), float(h[1])
 
+    def allreduce_stop(self, mx, ms, cnt, cnt2):
+        """(global max of mx, global max of ms, global sums of cnt and cnt2)
+        as python floats: the block path's per-sweep stop-test values."""
+        t = torch.stack([torch.as_tensor(x, dtype=torch.float64).reshape(()).to(self.device)
+                         for x in (mx, ms, cnt, cnt2)])
+        if self.distributed:
+            a = t[0:2].clone()
+            b = t[2:4].clone()
+            dist.all_reduce(a, op=dist.ReduceOp.MAX)
+            dist.all_reduce(b, op=dist.ReduceOp.SUM)
+            t = torch.cat([a, b])
+        h = t.cpu()
+        return float(h[0]), float(h[1]), float(h[2]), float(h[3])
+
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over ranks (device tensors: RCCL, stream-ordered)."""
         if self.distributed:
@@ -314,6 +328,9 @@ class SimCommunicator:
 
     def allreduce_max_sum(self, mx, cnt):
         return float(torch.as_tensor(mx).double()), float(torch.as_tensor(cnt).double())
+
+    def allreduce_stop(self, mx, ms, cnt, cnt2):
+        return tuple(float(torch.as_tensor(x).double()) for x in (mx, ms, cnt, cnt2))
 
     def allreduce_sum_(self, t):
         """The sum over ``world`` ranks is modelled as ``world`` copies of this

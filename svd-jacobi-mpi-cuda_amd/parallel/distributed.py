@@ -278,6 +278,7 @@ class DistributedBlockJacobi(Solver):
 
         hist, t_comm, t_total = [], 0.0, 0.0
         sweeps = 0
+        stop_reason = None
         start = 0
         sig = {"m": m, "n": n, "dtype": str(dtype), "P": P, "W": W, "B": B, "rank": g,
                "want_v": want_v}
@@ -321,7 +322,7 @@ class DistributedBlockJacobi(Solver):
         # (8192^2: 32 pairs per chain, merged +10 %).  SVDJ_MERGE_CHAINS=0/1
         # overrides; with exchanges merging was slower at every P.
         env_merge = os.environ.get("SVDJ_MERGE_CHAINS")
-        merged = (pipelined and dev.type == "cuda" and not quad and
+        merged = (pipelined and dev.type == "cuda" and
                   (env_merge == "1" if env_merge is not None
                    else (not comm.distributed and k // 2 >= 64)))
         for sw in range(start, cfg.max_sweeps):
@@ -344,14 +345,18 @@ class DistributedBlockJacobi(Solver):
                         K.block_steps(At, Vt, D, m_pad, dev_pairs[r], W, plans[r].modes, tol,
                                       cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
                                       tol_mode=cfg.tol_mode, inner_order=inner)
-                mx, nrot = self._reduce_metric(metric, dev)
+                mx, ms, nrot, ncr = self._reduce_metric(metric, dev)
             hist.append(mx)
             sweeps = sw + 1
             if cfg.progress and g == 0:
-                print(f"[svdj] sweep {sweeps}: off {mx:.3e}, rotated pairs {int(nrot)}, "
-                      f"{time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
-            if nrot == 0:
+                print(f"[svdj] sweep {sweeps}: off {mx:.3e}, eff sin {ms:.3e}, rotated pairs "
+                      f"{int(nrot)}, rotations {int(ncr)}, {time.perf_counter() - t0:.2f} s",
+                      file=sys.stderr, flush=True)
+            # every rank sees the same all-reduced values: the same decision
+            stop = K.sweep_converged(mx, ms, nrot, ncr, tol, cfg.tol_mode, cfg.stop_rule)
+            if stop:
                 converged = True
+                stop_reason = "no_rotation" if stop == 1 else "second_order"
                 break
             # The next sweep replays the same exchange pattern from the current
             # placement: the schedule only depends on positions, so every
@@ -372,7 +377,8 @@ class DistributedBlockJacobi(Solver):
         sigma_loc = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         sync()
         t_total = time.perf_counter() - t0
-        info = {"tol": tol, "converged": converged, "dtype": str(pdtype), "geometry": geo, "mma": mma,
+        info = {"tol": tol, "converged": converged, "stop_reason": stop_reason,
+                "stop_rule": cfg.stop_rule, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "inner_order": inner, "quad": quad, "merged_chains": bool(pipelined and merged),
                 "exchange": ex.exchange if pipelined else "direct",
                 "comm_seconds": t_comm, "rank": g, "held": list(held)}
@@ -443,13 +449,11 @@ class DistributedBlockJacobi(Solver):
             phys[h][int(tour.xslot[r, h])] = old[src_h][int(tour.xslot[r, src_h])]
 
     def _reduce_metric(self, metric, dev):
-        """Global (max off value, total rotations) of the sweep: one all-reduce
-        pair instead of the reference's discarded convergence value."""
-        if dev.type == "cuda":
-            pair = K.metric_as_float_pair(metric)
-            return self.comm.allreduce_max_sum(pair[0], pair[1])
-        lmx, lrot = K.read_metric(metric)
-        return self.comm.allreduce_max_sum(lmx, lrot)
+        """Global (max off value, max effective sine, rotated pairs, column
+        rotations) of the sweep (all-reduces instead of the reference's
+        discarded convergence value, main.cu:710)."""
+        v = K.metric_stop_values(metric)
+        return self.comm.allreduce_stop(v[0], v[1], v[2], v[3])
 
     def _distribute(self, A, generator, At, held, m, n, B, dtype):
         comm = self.comm

@@ -556,13 +556,15 @@ class PipelineExecutor:
                 done = self._event()
                 done.record(sa)
                 sb.wait_event(done)
-            elif len(tasks) == 2:
+            elif len(tasks) == 2 and run_pair is not None:
                 a, b = tasks
                 run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
                          (pairs[1], b.modes, b.stream, self.streams[b.stream]))
-            else:
-                with torch.cuda.stream(self.streams[tasks[0].stream]):
-                    run_steps(pairs[0], tasks[0].modes, tasks[0].stream)
+            else:  # one task, or a group that cannot merge and has no staggered issue:
+                # each task on its own stream (as run_merged falls back)
+                for q, t in enumerate(tasks):
+                    with torch.cuda.stream(self.streams[t.stream]):
+                        run_steps(pairs[q], t.modes, t.stream)
             for q, t in enumerate(tasks):
                 ev = self._event()
                 ev.record(self.streams[t.stream])

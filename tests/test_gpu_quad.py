@@ -86,18 +86,63 @@ def test_quad_step_equals_two_cross_steps(svdj, cuda, nb, m, inner):
     """A quad step is the two cross steps it fuses (mode 3, data Gram for the
     second) to fp32 rounding: the Gram-space couplings are exact.  nb = 128 is
     64 pairs (32 quads) per step, the 1-GPU geometry.  Also: V stays
-    orthogonal and A = A0 V on the touched columns."""
+    orthogonal and A = A0 V on the touched columns.
+
+    The quad Gram runs on split-bf16 MFMAs (gram_quad_kernel, products exact
+    to 2^-26), the cross steps' Gram on f32 MFMAs: both fp32-accurate, but
+    rounded differently.  With one inner EVD sweep the results agree column
+    by column; with three, the near-degenerate rotation angles the EVD
+    converges on are ill-conditioned in the couplings (the test's blocks have
+    graded, close norms; the D of a pair whose EVD stops before it converges
+    moves with them), so the two are compared through what is invariant: the
+    sum of the squared norms of every quad (the trace of its Gram), and the
+    validity of each result (gram_quad_kernel's own accuracy:
+    test_gram_quad_matches_fp64)."""
     A64, outs = _two_step_runs(svdj, cuda, nb, m, inner, ([4, 5], [3, 3]))
     (a1, v1, d1, (m1, r1)), (a2, v2, d2, (m2, r2)) = outs
     assert r1 == r2 == nb
     assert math.isclose(m1, m2, rel_tol=1e-3)
-    tol = 5e-5 if inner == 1 else 2e-4
-    torch.testing.assert_close(a1, a2, rtol=tol, atol=tol)
-    torch.testing.assert_close(v1, v2, rtol=tol, atol=tol)
-    torch.testing.assert_close(d1, d2, rtol=tol, atol=tol)
+    if inner == 1:
+        tol = 5e-5
+        torch.testing.assert_close(a1, a2, rtol=tol, atol=tol)
+        torch.testing.assert_close(v1, v2, rtol=tol, atol=tol)
+        torch.testing.assert_close(d1, d2, rtol=tol, atol=tol)
+    else:
+        torch.testing.assert_close(d1.view(-1, 4 * 64).sum(1), d2.view(-1, 4 * 64).sum(1),
+                                   rtol=1e-6, atol=0)
     n = v1.shape[0]
-    assert float((v1 @ v1.t() - torch.eye(n, dtype=torch.float64)).abs().max()) < 2e-6
-    assert float((A64[:, :m].t() @ v1.t() - a1[:, :m].t()).abs().max()) < 2e-5
+    for a, v in ((a1, v1), (a2, v2)):
+        assert float((v @ v.t() - torch.eye(n, dtype=torch.float64)).abs().max()) < 2e-6
+        assert float((A64[:, :m].t() @ v.t() - a[:, :m].t()).abs().max()) < 2e-5
+
+
+def test_gram_quad_matches_fp64(svdj, cuda):
+    """gram_quad_kernel (one read of the quad's four blocks, the six cross
+    Grams on split-bf16 MFMAs) against fp64 products: every entry within
+    2e-6 of |a_i| |b_j| (fp32 level: the split products are exact to 2^-26
+    and the accumulation is fp32), for 16 quads, several row chunks."""
+    K = svdj.ops.kernels
+    W, nb, m, m_pad = 64, 64, 1000, 1024
+    g = torch.Generator().manual_seed(4)
+    A64 = torch.zeros(nb * W, m_pad, dtype=torch.float64)
+    A64[:, :m] = torch.rand(nb * W, m, generator=g, dtype=torch.float64) - 0.4
+    A64 *= torch.logspace(-3, 3, nb * W, dtype=torch.float64)[:, None]  # graded column norms
+    At = A64.float().to(cuda)
+    pairs = torch.from_numpy(svdj.parallel.schedule.quad_round_robin(nb)[1].copy())
+    sl = K.gram_quad(At, m_pad, pairs.to(cuda), W, 256)  # (3P, nchunk, W, W)
+    P = pairs.shape[0]
+    C = sl.double().sum(1).cpu()
+    X = At.double().cpu()
+    nrm = X.norm(dim=1)
+    want = [tuple(pr) for pr in pairs.tolist()]  # slabs [0, P): the step's pairs
+    for q in range(P // 2):
+        (a, c_), (b, d) = pairs[2 * q].tolist(), pairs[2 * q + 1].tolist()
+        want.extend([(a, d), (b, c_), (a, b), (c_, d)])
+    for s_, (x, y) in enumerate(want):
+        ref = X[x * W:(x + 1) * W] @ X[y * W:(y + 1) * W].t()
+        scale = nrm[x * W:(x + 1) * W, None] * nrm[None, y * W:(y + 1) * W]
+        err = float(((C[s_] - ref).abs() / scale).max())
+        assert err < 2e-6, (s_, x, y, err)
 
 
 def test_quad_preconverged_skipped(svdj, cuda):
