@@ -158,6 +158,30 @@ def verify_rows(res, gen, m, n, comm, dtype):
             "orth_v_fro": float((V.t() @ V - eye).double().norm())}
 
 
+class _ticker:
+    """A stderr line every 30 s while a long silent call runs (the fp64
+    oracle), so a job watchdog does not take the run for hung."""
+
+    def __init__(self, what):
+        self.what = what
+
+    def __enter__(self):
+        import threading
+        self.t0, self.stop = time.time(), threading.Event()
+
+        def run():
+            while not self.stop.wait(30):
+                print(f"[bench] {self.what}: {time.time() - self.t0:.0f} s", file=sys.stderr,
+                      flush=True)
+        self.th = threading.Thread(target=run, daemon=True)
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+
+
 def sigma_check(res, gen, m, n, comm):  # noqa: C901
     """max |sigma - sigma_ref| / sigma_ref_max against an fp64 oracle
     (torch.linalg.svdvals of the regenerated A in fp64 on the device,
@@ -178,7 +202,10 @@ def sigma_check(res, gen, m, n, comm):  # noqa: C901
     if comm.rank != 0:
         return None
     A = gen(0, n).double()
-    ref = torch.linalg.svdvals(A)
+    with _ticker(f"sigma oracle: fp64 svdvals of {m}x{n}"):  # minutes at n >= 8192
+        ref = torch.linalg.svdvals(A)
+        if ref.is_cuda:
+            torch.cuda.synchronize()
     got = torch.sort(sig, descending=True).values
     return float((got - ref).abs().max() / ref[0])
 
@@ -393,6 +420,7 @@ def run_native(a, dtype, work):
     p.comm_timing = 1 if a.comm_timing else 0
     p.progress = 1 if a.progress else 0
     p.stop_rule = K.STOP_RULES[a.stop_rule]
+    p.quad = {"auto": 0, "on": 1, "off": 2}[a.quad]
     p.fault_rank, p.fault_sweep = -1, -1
     if a.inject_fault:
         p.fault_rank, p.fault_sweep = (int(x) for x in a.inject_fault.split(":"))
@@ -469,12 +497,18 @@ def run_native(a, dtype, work):
                            int(p.inner_order_used), a.inner_order),
                        "exchange": {1: "direct", 2: "spread"}.get(int(p.exchange_used), "direct"),
                        "staggered": bool(a.stagger), "root_owned": False,
+                       "quad_steps": bool(p.quad_used), "merged_chains": bool(p.merged_used),
                        "stop_rule": a.stop_rule},
             "sweeps": sweeps, "converged": conv, "stop_reason": sorted(reasons),
             "time_to_converge_s": round(ms / 1e3, 4),
             "off_history_last": [float("%.3e" % hist[i]) for i in range(max(0, p.sweeps - 3), p.sweeps)],
             "comm": ({"exchanges": int(p.exchanges), "bytes_sent": int(p.bytes_sent),
                       "timing": bool(a.comm_timing),
+                      **({"exchange_choice": (
+                          f"measured at handle creation: direct {p.calib_direct_ms:.3f} ms, spread "
+                          f"{p.calib_spread_ms:.3f} ms per half exchange -> "
+                          f"{'spread' if int(p.exchange_used) == 2 else 'direct'}")}
+                         if p.calib_direct_ms > 0 else {}),
                       **({"comm_ms": round(p.comm_ms, 3), "exposed_comm_ms": round(p.exposed_comm_ms, 3)}
                          if a.comm_timing else {})} if world > 1 else None),
             "world": world, "rccl_ranks": world,

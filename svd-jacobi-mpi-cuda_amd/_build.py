@@ -152,6 +152,31 @@ def build_dist(force: bool = False, verbose: bool = False) -> Path:
     return DIST_LIB
 
 
+ASAN_DIST_LIB = LIBDIR / "asan" / "libsvdj_dist.so"
+
+
+def build_dist_asan(force: bool = False, verbose: bool = False) -> Path:
+    """AddressSanitizer + UBSan build of libsvdj_dist's host code (id-file
+    handshake, plan and list builder, watchdog thread) into lib/asan/.  The
+    file holds no device code, so g++ compiles it against the HIP runtime
+    headers, with the same sanitizer runtime as ``build_cpu(asan=True)``;
+    it links the ASan libsvdj_cpu next to it and the regular libsvdj_hip.
+    Load with SVDJ_DIST_LIB=<path> (tools/asan_cpu_tests.sh)."""
+    cpu, hip = build_cpu(force, verbose, asan=True), build_hip(force, verbose)
+    target = ASAN_DIST_LIB
+    if not force and not _stale(target, [DIST_SRC, cpu, hip, Path(__file__)] + HEADERS):
+        return target
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = target.with_suffix(".so.tmp")
+    _run([os.environ.get("CXX", "g++"), "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+          "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__",
+          f"-I{rocm}/include", f"-I{CSRC / 'include'}", DIST_SRC, "-o", tmp,
+          f"-L{target.parent}", "-lsvdj_cpu", f"-L{LIBDIR}", "-lsvdj_hip", f"-L{rocm}/lib",
+          "-lamdhip64", "-lrccl", "-Wl,-rpath,$ORIGIN:$ORIGIN/.."], verbose)
+    os.replace(tmp, target)
+    return target
+
+
 def build_all(force: bool = False, verbose: bool = False) -> dict:
     return {"cpu": str(build_cpu(force, verbose)), "hip": str(build_hip(force, verbose)),
             "driver": str(build_driver(force, verbose)),

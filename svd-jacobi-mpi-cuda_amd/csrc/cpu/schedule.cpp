@@ -100,6 +100,46 @@ extern "C" int svdj_bipartite(int k, int32_t* out) {
   return k;
 }
 
+// Quad orders (csrc/hip/block.hip "quad step"; parallel/schedule.py twins):
+// two consecutive steps fuse over the four blocks (a, b, c, d) of a
+// super-block pair {a, b} x {c, d}: step s pairs (a, c), (b, d), step s+1
+// (a, d), (b, c), as pairs 2q, 2q+1 of quad q.
+extern "C" int svdj_quad_round_robin(int nb, int32_t* out) {
+  if (nb < 4 || nb % 4 || out == nullptr) return -1;
+  const int K = nb / 2;  // super-blocks (2i, 2i+1)
+  for (int i = 0; i < K; ++i) {  // step 0: within every super-block (the full-Gram step)
+    out[2 * i] = 2 * i;
+    out[2 * i + 1] = 2 * i + 1;
+  }
+  std::vector<int32_t> srr((size_t)(K - 1) * (K / 2) * 2);
+  svdj_round_robin(K, srr.data());
+  for (int t = 0; t < K - 1; ++t)
+    for (int q = 0; q < K / 2; ++q) {
+      const int I = srr[((size_t)t * (K / 2) + q) * 2], J = srr[((size_t)t * (K / 2) + q) * 2 + 1];
+      const int a = 2 * I, b = 2 * I + 1, c = 2 * J, d = 2 * J + 1;
+      int32_t* s1 = out + (size_t)(1 + 2 * t) * K * 2 + 4 * q;
+      int32_t* s2 = out + (size_t)(2 + 2 * t) * K * 2 + 4 * q;
+      s1[0] = a, s1[1] = c, s1[2] = b, s1[3] = d;
+      s2[0] = a, s2[1] = d, s2[2] = b, s2[3] = c;
+    }
+  return nb - 1;
+}
+
+extern "C" int svdj_quad_bipartite(int h, const int32_t* xs, const int32_t* ys, int32_t* out) {
+  if (h < 2 || h % 2 || !xs || !ys || !out) return -1;
+  const int H = h / 2;
+  for (int t = 0; t < H; ++t)
+    for (int i = 0; i < H; ++i) {
+      const int j = (i + t) % H;
+      const int a = xs[2 * i], b = xs[2 * i + 1], c = ys[2 * j], d = ys[2 * j + 1];
+      int32_t* s1 = out + (size_t)(2 * t) * h * 2 + 4 * i;
+      int32_t* s2 = out + (size_t)(2 * t + 1) * h * 2 + 4 * i;
+      s1[0] = a, s1[1] = c, s1[2] = b, s1[3] = d;
+      s2[0] = a, s2[1] = d, s2[2] = b, s2[3] = c;
+    }
+  return h;
+}
+
 extern "C" int svdj_tournament(int P, int32_t* held, int32_t* xslot,
                                int32_t* send_to, int32_t* recv_from) {
   if (P < 1 || held == nullptr) return -1;

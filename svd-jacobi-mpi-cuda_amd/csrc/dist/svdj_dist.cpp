@@ -3,7 +3,9 @@
 // (parallel/pipeline.py, parallel/distributed.py):
 //
 // Per sweep on GPU g (slots 0 and 1 hold super-blocks of k = B/W blocks,
-// each split in halves 0|1 of k/2 blocks; I = incoming slot, S = the other):
+// each split in halves 0|1 of k/2 blocks; I = incoming slot, S = the other;
+// one GPU from 64 pairs per chain step: the task pairs merged into single
+// launches of twice the pairs and quad steps, as the Python engine):
 //   round 0 : round robin inside each slot            (chain 0: slot 0, 1: slot 1)
 //   round r : I0xS0 (0), I0xS1 (0), I1xS0 (1), send half 0 of the slot
 //             replaced next, I1xS1 (1), send half 1   (last round: no sends)
@@ -126,47 +128,61 @@ std::string job_token() {
 }
 }  // namespace
 
-extern "C" int svdj_dist_comm_init(int rank, int world, const char* id_path, double timeout_s,
-                                   void** comm) {
+// Host part of the bootstrap (no RCCL, no GPU; CPU-tested under ASan):
+// rank 0 publishes `n` bytes at `path` (written to path.tmp, then renamed),
+// every other rank waits for a fresh file of this job's token and reads them.
+extern "C" int svdj_dist_id_file(int rank, const char* id_path, double timeout_s, void* blob,
+                                 size_t n) {
   IdFile rec;
+  if (n != sizeof(rec.id)) return fail(-2, "id blob of %zu bytes, expected %zu", n, sizeof(rec.id));
   std::memset(&rec, 0, sizeof(rec));
   const std::string path(id_path), token = job_token();
   if (rank == 0) {
-    NCCLC(ncclGetUniqueId(&rec.id));
+    std::memcpy(&rec.id, blob, n);
     std::memcpy(rec.magic, kIdMagic, sizeof(kIdMagic));
     std::memcpy(rec.token, token.data(), token.size());
     const std::string tmp = path + ".tmp";
     FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f || fwrite(&rec, sizeof(rec), 1, f) != 1) return fail(-1, "cannot write %s", tmp.c_str());
+    if (!f) return fail(-1, "cannot write %s", tmp.c_str());
+    const bool ok = fwrite(&rec, sizeof(rec), 1, f) == 1;
     fclose(f);
+    if (!ok) return fail(-1, "cannot write %s", tmp.c_str());
     if (rename(tmp.c_str(), path.c_str()) != 0) return fail(-1, "cannot publish %s", path.c_str());
-  } else {
-    const double window = token.empty() ? 30.0 : (timeout_s > 30 ? timeout_s : 30.0);
-    const time_t not_before = time(nullptr) - (time_t)window;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      struct stat sb;
-      const bool fresh = stat(path.c_str(), &sb) == 0 && sb.st_mtime >= not_before;
-      FILE* f = fresh ? fopen(path.c_str(), "rb") : nullptr;
-      if (f) {
-        IdFile got;
-        const size_t n = fread(&got, sizeof(got), 1, f);
-        fclose(f);
-        if (n == 1 && !std::memcmp(got.magic, kIdMagic, sizeof(kIdMagic)) &&
-            !std::strncmp(got.token, token.c_str(), sizeof(got.token))) {
-          rec = got;
-          break;
-        }
-      }
-      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > timeout_s)
-        return fail(-2, "rank %d: no unique id of this job (token '%s') at %s after %.0f s", rank,
-                    token.c_str(), path.c_str(), el);
-      std::this_thread::sleep_for(std::chrono::milliseconds(20));
-    }
+    return 0;
   }
+  const double window = token.empty() ? 30.0 : (timeout_s > 30 ? timeout_s : 30.0);
+  const time_t not_before = time(nullptr) - (time_t)window;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    struct stat sb;
+    const bool fresh = stat(path.c_str(), &sb) == 0 && sb.st_mtime >= not_before;
+    FILE* f = fresh ? fopen(path.c_str(), "rb") : nullptr;
+    if (f) {
+      IdFile got;
+      const size_t k = fread(&got, sizeof(got), 1, f);
+      fclose(f);
+      if (k == 1 && !std::memcmp(got.magic, kIdMagic, sizeof(kIdMagic)) &&
+          !std::strncmp(got.token, token.c_str(), sizeof(got.token))) {
+        std::memcpy(blob, &got.id, n);
+        return 0;
+      }
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > timeout_s)
+      return fail(-2, "rank %d: no unique id of this job (token '%s') at %s after %.0f s", rank,
+                  token.c_str(), path.c_str(), el);
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+}
+
+extern "C" int svdj_dist_comm_init(int rank, int world, const char* id_path, double timeout_s,
+                                   void** comm) {
+  ncclUniqueId id;
+  std::memset(&id, 0, sizeof(id));
+  if (rank == 0) NCCLC(ncclGetUniqueId(&id));
+  if (int r = svdj_dist_id_file(rank, id_path, timeout_s, &id, sizeof(id))) return r;
   ncclComm_t c;
-  NCCLC(ncclCommInitRank(&c, world, rec.id, rank));
+  NCCLC(ncclCommInitRank(&c, world, id, rank));
   *comm = c;
   return 0;
 }
@@ -477,6 +493,13 @@ struct svdj_dist_handle_t {
   uint32_t* metric = nullptr;
   int32_t* pairs_pool = nullptr;
   Template rr[2], cross[2][2][2];
+  bool quad = false;    // quad steps (two cross steps fused) in every template
+  bool merged = false;  // one GPU: each parallel task pair issued as one launch of twice the pairs
+  int32_t* merged_pairs = nullptr;  // [rr0+rr1 | T00+T11 | T01+T10], device
+  size_t merged_off[3] = {0, 0, 0};
+  int merged_steps[3] = {0, 0, 0}, merged_np[3] = {0, 0, 0};
+  std::vector<int32_t> merged_modes[3];
+  double calib_ms[2] = {0, 0};  // exchange calibration: direct, spread (0: not run)
   std::vector<Item> items;
   std::vector<Group> groups;
   // per item: end event (task) / arrival (send); timing: start (task) / issue
@@ -488,11 +511,19 @@ struct svdj_dist_handle_t {
 
 namespace {
 
-int build_templates(svdj_dist_handle_t* h, int cross_mode) {
+// Host part of the plan's pair lists: every template's pairs and modes and,
+// on one GPU, the merged lists (mp).  No device call (svdj_dist_merged_lists
+// exposes it to the CPU tests).
+void template_hosts(svdj_dist_handle_t* h, int cross_mode, std::vector<int32_t>& mp) {
   const int k = h->k, hk = h->hk;
   std::vector<int32_t> rr((size_t)(k - 1) * (k / 2) * 2);
-  svdj_round_robin(k, rr.data());
   std::vector<int32_t> rr_modes(k - 1, cross_mode);
+  if (h->quad) {  // quad order (block.hip "quad step"): modes 4 / 5 in pairs
+    svdj_quad_round_robin(k, rr.data());
+    for (int s = 1; s < k - 1; ++s) rr_modes[s] = (s & 1) ? 4 : 5;
+  } else {
+    svdj_round_robin(k, rr.data());
+  }
   rr_modes[0] = 1;  // the first step of a sweep re-measures the diagonal (full Gram)
   for (int s = 0; s < 2; ++s) {
     Template& t = h->rr[s];
@@ -510,17 +541,57 @@ int build_templates(svdj_dist_handle_t* h, int cross_mode) {
         const int stay = 1 - inc;
         Template& t = h->cross[inc][ih][sh];
         t.host.assign((size_t)hk * hk * 2, 0);
-        for (int q = 0; q < hk; ++q)
+        if (h->quad) {
+          std::vector<int32_t> xs(hk), ys(hk);
           for (int a = 0; a < hk; ++a) {
-            t.host[(q * hk + a) * 2] = inc * k + ih * hk + a;
-            t.host[(q * hk + a) * 2 + 1] = stay * k + sh * hk + (a + q) % hk;
+            xs[a] = inc * k + ih * hk + a;
+            ys[a] = stay * k + sh * hk + a;
           }
+          svdj_quad_bipartite(hk, xs.data(), ys.data(), t.host.data());
+          t.modes.assign(hk, 4);
+          for (int s = 1; s < hk; s += 2) t.modes[s] = 5;
+        } else {
+          for (int q = 0; q < hk; ++q)
+            for (int a = 0; a < hk; ++a) {
+              t.host[(q * hk + a) * 2] = inc * k + ih * hk + a;
+              t.host[(q * hk + a) * 2 + 1] = stay * k + sh * hk + (a + q) % hk;
+            }
+          t.modes.assign(hk, cross_mode);
+        }
         t.steps = hk;
         t.npairs = hk;
-        t.modes.assign(hk, cross_mode);
         t.hv[0] = inc * 2 + ih;
         t.hv[1] = stay * 2 + sh;
       }
+  mp.clear();
+  if (h->merged) {
+    // one GPU (canonical buffers: a local block id is its buffer block):
+    // the parallel task pairs of the sweep -- rr0 + rr1, then the last round's
+    // [T00 || T11] and [T01 || T10] -- concatenated step by step, the order
+    // of pipeline.run_merged
+    const Template* grp[3][2] = {{&h->rr[0], &h->rr[1]},
+                                 {&h->cross[0][0][0], &h->cross[0][1][1]},
+                                 {&h->cross[0][0][1], &h->cross[0][1][0]}};
+    for (int m = 0; m < 3; ++m) {
+      const Template &x = *grp[m][0], &y = *grp[m][1];
+      h->merged_off[m] = mp.size();
+      h->merged_steps[m] = x.steps;
+      h->merged_np[m] = x.npairs + y.npairs;
+      h->merged_modes[m] = x.modes;
+      for (int st = 0; st < x.steps; ++st) {
+        mp.insert(mp.end(), x.host.begin() + (size_t)st * x.npairs * 2,
+                  x.host.begin() + (size_t)(st + 1) * x.npairs * 2);
+        mp.insert(mp.end(), y.host.begin() + (size_t)st * y.npairs * 2,
+                  y.host.begin() + (size_t)(st + 1) * y.npairs * 2);
+      }
+    }
+  }
+}
+
+int build_templates(svdj_dist_handle_t* h, int cross_mode) {
+  const int k = h->k, hk = h->hk;
+  std::vector<int32_t> mp;
+  template_hosts(h, cross_mode, mp);
   // every placement of each template's two halves: half h lives in one of
   // buffers {h, 2+h, 4+h} (only the canonical ones on one GPU)
   std::vector<Template*> all = {&h->rr[0], &h->rr[1]};
@@ -548,8 +619,41 @@ int build_templates(svdj_dist_handle_t* h, int cross_mode) {
   HIPC(hipMalloc((void**)&h->pairs_pool, pool.size() * sizeof(int32_t)));
   HIPC(hipMemcpy(h->pairs_pool, pool.data(), pool.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   for (auto& w : where) std::get<0>(w)->dev[std::get<1>(w)][std::get<2>(w)] = h->pairs_pool + std::get<3>(w);
+  if (h->merged) {
+    HIPC(hipMalloc((void**)&h->merged_pairs, mp.size() * sizeof(int32_t)));
+    HIPC(hipMemcpy(h->merged_pairs, mp.data(), mp.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   return 0;
 }
+
+}  // namespace
+
+extern "C" int svdj_dist_merged_lists(int k, int quad, int cross_mode, int32_t* pairs, int pcap,
+                                      int32_t* modes, int mcap, int32_t* meta) {
+  if (k < 4 || k % 2 || (quad && k % 4)) return fail(-2, "bad merged-list args");
+  svdj_dist_handle_t h{};
+  h.rank = 0;
+  h.world = 1;
+  h.k = k;
+  h.hk = k / 2;
+  h.quad = quad != 0;
+  h.merged = true;
+  std::vector<int32_t> mp;
+  template_hosts(&h, cross_mode, mp);
+  size_t nm = 0;
+  for (int m = 0; m < 3; ++m) nm += h.merged_modes[m].size();
+  if (mp.size() > (size_t)pcap || nm > (size_t)mcap) return fail(-3, "merged lists: buffer too small");
+  std::copy(mp.begin(), mp.end(), pairs);
+  for (int m = 0, at = 0; m < 3; ++m) {
+    meta[m * 3] = (int32_t)h.merged_off[m];
+    meta[m * 3 + 1] = h.merged_steps[m];
+    meta[m * 3 + 2] = h.merged_np[m];
+    for (int32_t v : h.merged_modes[m]) modes[at++] = v;
+  }
+  return (int)mp.size();
+}
+
+namespace {
 
 void handle_free(svdj_dist_handle_t* h) {
   if (!h) return;
@@ -560,12 +664,157 @@ void handle_free(svdj_dist_handle_t* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->own_sc && h->sc) (void)hipStreamDestroy(h->sc);
   (void)hipFree(h->pairs_pool);
+  (void)hipFree(h->merged_pairs);
   (void)hipFree(h->relay[0]);
   (void)hipFree(h->relay[1]);
   (void)hipFree(h->ws[0]);
   (void)hipFree(h->ws[1]);
   (void)hipFree(h->metric);
   delete h;
+}
+
+
+// One half exchange of tournament round `round` on stream sc (grouped RCCL):
+// each message goes to send_to and arrives from recv_from, directly, or
+// (spread, a message with a relay buffer) cut into P-1 near-equal chunks --
+// chunk 0 direct, chunk j >= 1 via the j-th rank not in {sender, receiver}
+// -- in two grouped phases (parallel/spread.py).  The data that arrives is
+// the same bit for bit.
+struct XMsg {
+  char *out, *in;
+  size_t n;
+  char* relay;  // non-null: relayed (spread)
+  size_t relay_n;
+};
+int exchange_ops(const Tour& tour, int round, int g, const XMsg* msgs, int nm, bool spread,
+                 ncclDataType_t nt, size_t es, ncclComm_t comm, hipStream_t sc) {
+  const int P = tour.P, dst = tour.to(round, g), src = tour.from(round, g);
+  auto piece = [&](size_t n, int j, size_t& a, size_t& len) {
+    const size_t base = n / (P - 1), rem = n % (P - 1);
+    a = j * base + ((size_t)j < rem ? (size_t)j : rem);
+    len = base + ((size_t)j < rem ? 1 : 0);
+  };
+  auto relay_index = [&](int s, int d, int q) {
+    int j = 0;
+    for (int x = 0; x < P; ++x) {
+      if (x == s || x == d) continue;
+      ++j;
+      if (x == q) return j;
+    }
+    return -1;
+  };
+  size_t a0, ln;
+  NCCLC(ncclGroupStart());  // direct messages / phase 1
+  for (int i = 0; i < nm; ++i) {
+    const XMsg& M = msgs[i];
+    if (!spread || !M.relay) {
+      NCCLC(ncclSend(M.out, M.n, nt, dst, comm, sc));
+      NCCLC(ncclRecv(M.in, M.n, nt, src, comm, sc));
+      continue;
+    }
+    piece(M.n, 0, a0, ln);
+    NCCLC(ncclSend(M.out + a0 * es, ln, nt, dst, comm, sc));
+    for (int q = 0, j = 0; q < P; ++q) {
+      if (q == g || q == dst) continue;
+      piece(M.n, ++j, a0, ln);
+      NCCLC(ncclSend(M.out + a0 * es, ln, nt, q, comm, sc));
+    }
+    piece(M.n, 0, a0, ln);
+    NCCLC(ncclRecv(M.in + a0 * es, ln, nt, src, comm, sc));
+    for (int s = 0; s < P; ++s) {  // sources this rank relays for
+      if (s == g || s == src) continue;
+      piece(M.n, relay_index(s, tour.to(round, s), g), a0, ln);
+      NCCLC(ncclRecv(M.relay + (size_t)s * M.relay_n * es, ln, nt, s, comm, sc));
+    }
+  }
+  NCCLC(ncclGroupEnd());
+  if (spread) {  // phase 2: forward the relayed chunks, receive ours
+    NCCLC(ncclGroupStart());
+    for (int i = 0; i < nm; ++i) {
+      const XMsg& M = msgs[i];
+      if (!M.relay) continue;
+      for (int s = 0; s < P; ++s) {
+        if (s == g || s == src) continue;
+        const int d = tour.to(round, s);
+        piece(M.n, relay_index(s, d, g), a0, ln);
+        NCCLC(ncclSend(M.relay + (size_t)s * M.relay_n * es, ln, nt, d, comm, sc));
+      }
+      for (int q = 0, j = 0; q < P; ++q) {
+        if (q == src || q == g) continue;
+        piece(M.n, ++j, a0, ln);
+        NCCLC(ncclRecv(M.in + a0 * es, ln, nt, q, comm, sc));
+      }
+    }
+    NCCLC(ncclGroupEnd());
+  }
+  return 0;
+}
+
+// Exchange calibration (pipeline.calibrate_exchange, ADVICE r3 / VERDICT r4):
+// at handle creation, from 4 ranks with exchange auto, one half exchange of
+// the first tournament round is timed both ways on this job's links (real
+// half-buffer sizes of A, the norms and V; one warm-up, the best of 3; every
+// timing the max over ranks), and spread is kept only if it is >= 10 %
+// faster.  Every rank takes the same decision (the times are all-reduced).
+int calibrate_exchange(svdj_dist_handle_t* h) {
+  const int P = h->world, g = h->rank;
+  Tour tour(P);
+  const size_t es = h->es;
+  const ncclDataType_t nt = h->dtype == 1 ? ncclFloat64 : ncclFloat32;
+  const size_t n[3] = {(size_t)h->hB * h->m_pad, (size_t)h->hB, h->has_v ? (size_t)h->hB * h->n_v : 0};
+  char* buf[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};
+  double* dt = nullptr;
+  int rc = 0;
+  for (int i = 0; i < 3 && !rc; ++i)
+    for (int j = 0; j < 2 && !rc && n[i]; ++j)
+      if (hipMalloc((void**)&buf[i][j], n[i] * es) != hipSuccess || hipMemset(buf[i][j], 0, n[i] * es) != hipSuccess)
+        rc = fail(-100, "calibration buffers: hipMalloc failed");
+  if (!rc && hipMalloc((void**)&dt, sizeof(double)) != hipSuccess) rc = fail(-100, "hipMalloc failed");
+  double best[2] = {1e30, 1e30};
+  for (int v = 0; v < 2 && !rc; ++v) {
+    const bool spread = v == 1;
+    XMsg msgs[3];
+    int nm = 0;
+    msgs[nm++] = {buf[0][0], buf[0][1], n[0], spread ? (char*)h->relay[0] : nullptr, h->relay_n[0]};
+    msgs[nm++] = {buf[1][0], buf[1][1], n[1], nullptr, 0};
+    if (n[2]) msgs[nm++] = {buf[2][0], buf[2][1], n[2], spread ? (char*)h->relay[1] : nullptr, h->relay_n[1]};
+    for (int it = 0; it < 4 && !rc; ++it) {
+      // line the ranks up (a tiny all-reduce), then time one exchange
+      if (ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess ||
+          hipStreamSynchronize(h->sc) != hipSuccess) {
+        rc = fail(-200, "calibration barrier failed");
+        break;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      if ((rc = exchange_ops(tour, 1, g, msgs, nm, spread, nt, es, h->comm, h->sc))) break;
+      if (hipStreamSynchronize(h->sc) != hipSuccess) {
+        rc = fail(-100, "calibration sync failed");
+        break;
+      }
+      double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (hipMemcpy(dt, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
+          ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess ||
+          hipStreamSynchronize(h->sc) != hipSuccess ||
+          hipMemcpy(&t, dt, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) {
+        rc = fail(-200, "calibration max over ranks failed");
+        break;
+      }
+      if (it) best[v] = std::min(best[v], t);
+    }
+  }
+  for (auto& b : buf)
+    for (char* x : b) (void)hipFree(x);
+  (void)hipFree(dt);
+  if (rc) return rc;
+  h->calib_ms[0] = best[0] * 1e3;
+  h->calib_ms[1] = best[1] * 1e3;
+  h->spread = best[1] < 0.9 * best[0];
+  if (!h->spread)
+    for (void*& r : h->relay) {
+      (void)hipFree(r);
+      r = nullptr;
+    }
+  return 0;
 }
 
 }  // namespace
@@ -592,8 +841,17 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   // 3 = auto: by the pairs of a cross step (half super-blocks)
   const int io = p->inner_order == 3 ? svdj_choose_inner_order(p->dtype, W, h->hk) : p->inner_order;
   h->io = io;
-  guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
-  h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->k / 2, p->m_pad, 0);
+  // one GPU from 64 pairs per chain step: merged issue, quad steps by default
+  // (the Python engine's rules: distributed.py merged, models/block.py choose_quad)
+  const char* em = getenv("SVDJ_MERGE_CHAINS");
+  h->merged = p->world == 1 && (em ? atoi(em) == 1 : h->hk >= 64);
+  const bool quad_ok = p->dtype == 0 && W == 64 && (p->mma == 1 || p->mma == 2) && h->k % 4 == 0;
+  if (p->quad < 0 || p->quad > 2) rc = fail(-2, "quad %d (0 auto, 1 on, 2 off)", p->quad);
+  if (p->quad == 1 && !quad_ok) rc = rc ? rc : fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
+  h->quad = quad_ok && (p->quad == 1 || (p->quad == 0 && p->world == 1 && h->hk >= 64));
+  if (!rc) guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
+  h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->merged ? h->k : h->k / 2, p->m_pad,
+                                      h->quad ? 1 : 0);
   for (int c = 0; c < 2 && !rc; ++c)
     if (hipMalloc(&h->ws[c], h->wsb) != hipSuccess) rc = fail(-100, "hipMalloc(ws %zu) failed", h->wsb);
   if (!rc && hipMalloc((void**)&h->metric, SVDJ_METRIC_WORDS * sizeof(uint32_t)) != hipSuccess)
@@ -614,6 +872,7 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
     else
       h->own_sc = true;
   }
+  if (!rc && h->world >= 4 && p->exchange == 0) guard(calibrate_exchange(h));
   if (rc) {
     handle_free(h);
     return rc;
@@ -754,6 +1013,14 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     int halves_sent = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> sp_busy, sp_wait, sp_span;
     if (svdj_reset_metric(h->metric, sa) != 0) return fail(-100, "metric reset failed");
+    if (h->merged) {  // one GPU: three merged launches on one stream, nothing to wait for
+      for (int m = 0; m < 3; ++m)
+        SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
+                               h->merged_pairs + h->merged_off[m], h->merged_np[m],
+                               h->merged_steps[m], h->merged_modes[m].data(), p->tol, p->tol_mode,
+                               1, h->ws[0], h->wsb, h->metric, p->mma, sa));
+      return 0;
+    }
     if (h->timing) HIPC(hipEventRecord(h->ev_t0, sa));
     HIPC(hipEventRecord(h->ev_join, sa));
     HIPC(hipStreamWaitEvent(st[1], h->ev_join, 0));
@@ -761,7 +1028,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     for (const Group& gr : groups) {
       const Item& a = items[gr.a];
       if (a.send) {  // one half of slot a.slot to send_to, its replacement from recv_from
-        const int key = a.slot * 2 + a.half, dst = tour.to(a.round, g), src = tour.from(a.round, g);
+        const int key = a.slot * 2 + a.half;
         const int out_b = L.loc[a.slot][a.half], in_b = L.spare[a.half];
         for (hipEvent_t e : last[key]) HIPC(hipStreamWaitEvent(sc, e, 0));
         last[key].clear();
@@ -769,12 +1036,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         std::unique_lock<std::mutex> lk(wd.mu);
         if (wd.fired.load()) return fail(-300, "%s", wd.why);
         // messages in the order of pipeline.py: A half, norms, V half
-        struct Msg {
-          char *out, *in;
-          size_t n;
-          char* relay;  // non-null: spread
-          size_t relay_n;
-        } msgs[3];
+        XMsg msgs[3];
         int nm = 0;
         msgs[nm++] = {buf_ptr(p->At, h->m_pad, out_b), buf_ptr(p->At, h->m_pad, in_b),
                       (size_t)hB * h->m_pad, h->spread ? (char*)h->relay[0] : nullptr, h->relay_n[0]};
@@ -784,68 +1046,9 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
           msgs[nm++] = {buf_ptr(p->Vt, h->n_v, out_b), buf_ptr(p->Vt, h->n_v, in_b),
                         (size_t)hB * h->n_v, h->spread ? (char*)h->relay[1] : nullptr,
                         h->relay_n[1]};
-        // spread (parallel/spread.py): chunk j of P-1 near-equal pieces; chunk 0
-        // direct, chunk j >= 1 via the j-th rank not in {sender, receiver}
-        auto piece = [&](size_t n, int j, size_t& a, size_t& len) {
-          const size_t base = n / (P - 1), rem = n % (P - 1);
-          a = j * base + ((size_t)j < rem ? (size_t)j : rem);
-          len = base + ((size_t)j < rem ? 1 : 0);
-        };
-        auto relay_index = [&](int s, int d, int q) {
-          int j = 0;
-          for (int x = 0; x < P; ++x) {
-            if (x == s || x == d) continue;
-            ++j;
-            if (x == q) return j;
-          }
-          return -1;
-        };
-        size_t a0, ln;
         ++n_exch;
         for (int i = 0; i < nm; ++i) n_bytes += (long long)msgs[i].n * (long long)es;
-        NCCLC(ncclGroupStart());  // direct messages / phase 1
-        for (int i = 0; i < nm; ++i) {
-          const Msg& M = msgs[i];
-          if (!M.relay) {
-            NCCLC(ncclSend(M.out, M.n, nt, dst, comm, sc));
-            NCCLC(ncclRecv(M.in, M.n, nt, src, comm, sc));
-            continue;
-          }
-          piece(M.n, 0, a0, ln);
-          NCCLC(ncclSend(M.out + a0 * es, ln, nt, dst, comm, sc));
-          for (int q = 0, j = 0; q < P; ++q) {
-            if (q == g || q == dst) continue;
-            piece(M.n, ++j, a0, ln);
-            NCCLC(ncclSend(M.out + a0 * es, ln, nt, q, comm, sc));
-          }
-          piece(M.n, 0, a0, ln);
-          NCCLC(ncclRecv(M.in + a0 * es, ln, nt, src, comm, sc));
-          for (int s = 0; s < P; ++s) {  // sources this rank relays for
-            if (s == g || s == src) continue;
-            piece(M.n, relay_index(s, tour.to(a.round, s), g), a0, ln);
-            NCCLC(ncclRecv(M.relay + (size_t)s * M.relay_n * es, ln, nt, s, comm, sc));
-          }
-        }
-        NCCLC(ncclGroupEnd());
-        if (h->spread) {  // phase 2: forward the relayed chunks, receive ours
-          NCCLC(ncclGroupStart());
-          for (int i = 0; i < nm; ++i) {
-            const Msg& M = msgs[i];
-            if (!M.relay) continue;
-            for (int s = 0; s < P; ++s) {
-              if (s == g || s == src) continue;
-              const int d = tour.to(a.round, s);
-              piece(M.n, relay_index(s, d, g), a0, ln);
-              NCCLC(ncclSend(M.relay + (size_t)s * M.relay_n * es, ln, nt, d, comm, sc));
-            }
-            for (int q = 0, j = 0; q < P; ++q) {
-              if (q == src || q == g) continue;
-              piece(M.n, ++j, a0, ln);
-              NCCLC(ncclRecv(M.in + a0 * es, ln, nt, q, comm, sc));
-            }
-          }
-          NCCLC(ncclGroupEnd());
-        }
+        if (int r = exchange_ops(tour, a.round, g, msgs, nm, h->spread, nt, es, comm, sc)) return r;
         lk.unlock();
         // received in place: from here on (issue order) the half lives in in_b;
         // in_b's last readers were waited for by the exchange that freed it
@@ -952,6 +1155,10 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     return fail(-200, "norm floor all-reduce failed");
   p->inner_order_used = h->io;
   p->exchange_used = P > 1 ? (h->spread ? 2 : 1) : 0;
+  p->quad_used = h->quad ? 1 : 0;
+  p->merged_used = h->merged ? 1 : 0;
+  p->calib_direct_ms = h->calib_ms[0];
+  p->calib_spread_ms = h->calib_ms[1];
   const auto t_solve = std::chrono::steady_clock::now();
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
     if ((rc = sweep())) break;

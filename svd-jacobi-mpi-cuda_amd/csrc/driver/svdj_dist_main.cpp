@@ -6,7 +6,8 @@
 //   svdj_dist_main N --np P [--m M] [--input triu|dense] [--seed S]
 //                  [--dtype f32|f64] [--block W (default: per-GPU size)] [--max-sweeps K] [--tol T]
 //                  [--abs-tol] [--mma auto|native|bf16x6|bf16x3] [--inner auto|cyclic|bipartite|cross]
-//                  [--exchange auto|direct|spread] [--stop-rule second_order|no_rotation] [--no-v]
+//                  [--exchange auto|direct|spread] [--stop-rule second_order|no_rotation]
+//                  [--quad auto|on|off] [--no-v]
 //                  [--shared-gpu] [--verify] [--warmup K] [--timeout SEC]
 //                  [--id-file PATH] [--comm-timing] [--progress] [--inject-fault RANK:SWEEP] [--keep-going]
 //
@@ -58,6 +59,7 @@ struct Opts {
   int n = 0, m = 0, np = 0, W = 0, max_sweeps = 60, mma = 0, warmup = 0, inner = 3;  // auto
   int exchange = 0;  // auto
   int stop_rule = 1;  // second_order (svdj_stop.h)
+  int quad = 0;       // auto
   int fault_rank = -1, fault_sweep = -1;
   unsigned seed = 1000000;
   double tol = -1, timeout = 600;
@@ -168,6 +170,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   p.inner_order = o.inner;
   p.exchange = o.exchange;
   p.stop_rule = o.stop_rule;
+  p.quad = o.quad;
   p.stream_a = sa;
   p.stream_b = sb;
   p.stream_comm = sc;
@@ -224,6 +227,12 @@ int run_rank(const Opts& o, int rank, int world, int device) {
                 p.converged, p.sweeps > 0 ? hist[p.sweeps - 1] : 0.0, tol);
     const double flops = (double)n * (n - 1) / 2.0 * (12.0 * m + (o.want_v ? 6.0 * n : 0.0)) * p.sweeps;
     std::printf("GFLOP/s (algorithmic): %.1f\n", flops / secs / 1e9);
+    std::printf("issue: %s%s  exchange: %s\n", p.merged_used ? "merged chains" : "two chains",
+                p.quad_used ? ", quad steps" : "",
+                world == 1 ? "none" : (p.exchange_used == 2 ? "spread" : "direct"));
+    if (p.calib_direct_ms > 0)
+      std::printf("exchange calibration: direct %.3f ms, spread %.3f ms per half exchange\n",
+                  p.calib_direct_ms, p.calib_spread_ms);
     if (o.comm_timing)
       std::printf("comm_ms: %.3f  exposed_comm_ms: %.3f\n", p.comm_ms, p.exposed_comm_ms);
   }
@@ -384,6 +393,10 @@ int main(int argc, char** argv) {
     else if (a == "--comm-timing") o.comm_timing = true;
     else if (a == "--progress") o.progress = true;
     else if (a == "--stop-rule") o.stop_rule = std::string(next()) == "no_rotation" ? 0 : 1;
+    else if (a == "--quad") {
+      const std::string v = next();
+      o.quad = v == "on" ? 1 : (v == "off" ? 2 : 0);
+    }
     else if (a == "--keep-going") o.keep_going = true;
     else if (a == "--inject-fault") {
       const std::string v = next();

@@ -38,6 +38,15 @@ int svdj_round_robin(int nb, int32_t* out);
 // step t pairs (a, k + (a+t) mod k).  out[k][k][2].  Returns k.
 int svdj_bipartite(int k, int32_t* out);
 
+// Quad orders (two steps fused over the four blocks of a super-block pair
+// {a, b} x {c, d}: step s pairs (a, c), (b, d), step s+1 (a, d), (b, c) as
+// pairs 2q, 2q+1).  svdj_quad_round_robin: out[nb-1][nb/2][2], nb % 4 == 0,
+// step 0 the within-super-block pairs (2i, 2i+1), then a round robin over the
+// nb/2 super-blocks, two steps each.  svdj_quad_bipartite: out[h][h][2], the
+// cross pairs of block lists xs, ys (h even).  Return the step count or -1.
+int svdj_quad_round_robin(int nb, int32_t* out);
+int svdj_quad_bipartite(int h, const int32_t* xs, const int32_t* ys, int32_t* out);
+
 // Multi-GPU super-block tournament: 2P super-blocks, 2P-1 rounds, one pair per
 // GPU per round; between consecutive rounds every GPU replaces exactly one of
 // its two super-blocks (one send + one recv per GPU per round).

@@ -26,6 +26,11 @@ extern "C" {
 // (up to timeout_s).  The caller has selected the rank's device first.
 // *comm receives an ncclComm_t.  Returns 0 or <0.
 int svdj_dist_comm_init(int rank, int world, const char* id_path, double timeout_s, void** comm);
+// Its host part (no RCCL): rank 0 publishes the n-byte id (n = sizeof
+// ncclUniqueId) with this job's token (SVDJ_JOB_TOKEN, or TORCHELASTIC_RUN_ID
+// + TORCHELASTIC_RESTART_COUNT); other ranks accept only a fresh file (younger
+// than timeout_s with a token, 30 s without) carrying the same token.
+int svdj_dist_id_file(int rank, const char* id_path, double timeout_s, void* blob, size_t n);
 int svdj_dist_comm_destroy(void* comm);
 
 // Geometry of an m x n problem (m >= n) on `world` GPUs with block width W:
@@ -67,10 +72,12 @@ typedef struct {
                               // (svdj_choose_inner_order of the half super-block pairs)
   int stagger;                // 1: the two chains of a group offset by an EVD
                               // (svdj_block_steps2); 0 (default): issued independently
-  int exchange;               // half super-block transfer: 0 auto (spread from 4 ranks),
-                              // 1 direct (one grouped send/recv, one xGMI link), 2 spread
-                              // (P-1 chunks relayed over all links in two grouped phases,
-                              // parallel/spread.py)
+  int exchange;               // half super-block transfer: 0 auto (from 4 ranks both are
+                              // timed on the job's links when the handle is created and
+                              // spread is kept only if >= 10 % faster, as
+                              // pipeline.calibrate_exchange), 1 direct (one grouped
+                              // send/recv, one xGMI link), 2 spread (P-1 chunks relayed over
+                              // all links in two grouped phases, parallel/spread.py)
   void* stream_a;             // two compute streams (distinct)
   void* stream_b;
   void* stream_comm;          // exchange stream, or NULL (created by the handle).  HIP maps
@@ -96,6 +103,14 @@ typedef struct {
   int stop_rule;              // 1: a sweep also ends the iteration by the second-order rule
                               // (svdj_stop.h; relative mode); 0: only a sweep without
                               // rotations does.  converged (out) = 1 (no rotation) or 2
+  int quad;                   // quad steps (two cross steps fused, fp32 W = 64 split-bf16
+                              // apply): 0 auto (one GPU, >= 64 pairs per chain step:
+                              // models/block.py choose_quad), 1 on, 2 off
+  int quad_used;              // out
+  int merged_used;            // out: 1 = one GPU, the two chains issued as single launches of
+                              // twice the pairs (pipeline.run_merged; >= 64 pairs per chain step)
+  double calib_direct_ms;     // out: exchange calibration (exchange auto from 4 GPUs, at
+  double calib_spread_ms;     // handle creation): max over ranks of one half exchange, or 0
 } svdj_dist_problem;
 
 // Persistent per-rank state for repeated solves of one geometry: workspaces,
@@ -118,6 +133,14 @@ int svdj_dist_solve(svdj_dist_problem* p, void* sigma);
 // {stream, half, half, stream, half, half}, 2 = a half exchange {round, slot,
 // half}; halves are slot*2 + half.  Returns the group count (<= cap) or <0.
 int svdj_dist_plan(int world, int rank, int32_t* out, int cap);
+
+// One-GPU merged issue (host only, for tests): the pair lists of the three
+// merged task groups of a sweep with k blocks per super-block (rr0+rr1,
+// T00+T11, T01+T10; local block ids), concatenated step by step; modes[] the
+// step modes of each group in turn, meta[3][3] {offset, steps, pairs/step}.
+// Returns the number of ints written to pairs, or <0.
+int svdj_dist_merged_lists(int k, int quad, int cross_mode, int32_t* pairs, int pcap,
+                           int32_t* modes, int mcap, int32_t* meta);
 
 // Message of the calling thread's last failure.
 const char* svdj_dist_last_error(void);

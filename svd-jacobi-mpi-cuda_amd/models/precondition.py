@@ -83,6 +83,14 @@ def _cholqr2(A: torch.Tensor):
     return Q1, L2.t() @ L1.t(), L2.t()
 
 
+def _ordered_sum(G: torch.Tensor, comm) -> torch.Tensor:
+    """sum_g G_g added in rank order on every rank (bitwise the same result
+    whatever the backend); communicators without it (the one-GPU plan
+    simulator's cost model) all-reduce."""
+    f = getattr(comm, "ordered_sum_", None)
+    return f(G) if f is not None else comm.allreduce_sum_(G)
+
+
 def dist_qr(A_loc: torch.Tensor, dtype: torch.dtype, comm):
     """Row-distributed CholeskyQR2: rank g holds rows A_g (m_g x n) of A.
 
@@ -95,12 +103,18 @@ def dist_qr(A_loc: torch.Tensor, dtype: torch.dtype, comm):
     The QR cost is divided by P; the replicated m x n factorisation it
     replaces was redundant work on every rank.
 
+    The two Gram sums are rank-ordered (all-gather, then G_0 + G_1 + ... on
+    every rank): a floating all-reduce adds in an order that depends on the
+    backend and the ring (RCCL and gloo differ), which changes R's low bits
+    and with them every later bit of the solve.  At BASELINE config 4
+    (n = 8192, P = 4) that is 768 MB gathered per rank instead of 384 MB
+    all-reduced -- a few ms over xGMI next to a ~180 ms QR.
+
     Returns (Q1_g, R, L2^T), or None when a Gram is not numerically positive
     definite (kappa(A) >~ eps^-1/2) -- the same decision on every rank."""
     A = A_loc.to(dtype)
     eps = torch.finfo(dtype).eps
-    G = A.t() @ A
-    comm.allreduce_sum_(G)
+    G = _ordered_sum(A.t() @ A, comm)
     L1, info = torch.linalg.cholesky_ex(G)
     if int(info) != 0 or not bool(torch.isfinite(L1).all()):
         return None
@@ -108,8 +122,7 @@ def dist_qr(A_loc: torch.Tensor, dtype: torch.dtype, comm):
     if float(d.min()) <= eps ** 0.5 * float(d.max()):
         return None
     Q1 = torch.linalg.solve_triangular(L1.t(), A, upper=True, left=False)  # A L1^-T
-    G = Q1.t() @ Q1
-    comm.allreduce_sum_(G)
+    G = _ordered_sum(Q1.t() @ Q1, comm)
     L2, info = torch.linalg.cholesky_ex(G)
     if int(info) != 0 or not bool(torch.isfinite(L2).all()):
         return None

@@ -67,6 +67,8 @@ def cpu_lib():
         _sig(lib, "svdj_sameh_schedule", c_int, [c_int, c_i32_p])
         _sig(lib, "svdj_round_robin", c_int, [c_int, c_i32_p])
         _sig(lib, "svdj_bipartite", c_int, [c_int, c_i32_p])
+        _sig(lib, "svdj_quad_round_robin", c_int, [c_int, c_i32_p])
+        _sig(lib, "svdj_quad_bipartite", c_int, [c_int, c_i32_p, c_i32_p, c_i32_p])
         _sig(lib, "svdj_tournament", c_int, [c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
         for name, ptr in (("svdj_cpu_jacobi_f64", C.POINTER(C.c_double)),
                           ("svdj_cpu_jacobi_f32", C.POINTER(C.c_float))):
@@ -154,7 +156,9 @@ class DistProblem(C.Structure):
                 ("converged", c_int), ("comm_ms", c_double), ("exposed_comm_ms", c_double),
                 ("exchanges", C.c_longlong), ("bytes_sent", C.c_longlong),
                 ("progress", c_int), ("inner_order_used", c_int), ("exchange_used", c_int),
-                ("stop_rule", c_int)]
+                ("stop_rule", c_int), ("quad", c_int), ("quad_used", c_int),
+                ("merged_used", c_int), ("calib_direct_ms", c_double),
+                ("calib_spread_ms", c_double)]
 
 
 def dist_lib_path() -> Path:
@@ -162,6 +166,9 @@ def dist_lib_path() -> Path:
     the shared object, never the ``bin/svdj_dist_main`` launcher."""
     from .. import _build
 
+    override = os.environ.get("SVDJ_DIST_LIB")  # e.g. the host-ASan build
+    if override:
+        return Path(override)
     if os.environ.get("SVDJ_NO_AUTOBUILD") != "1":
         _build.build_dist()
     return _build.DIST_LIB
@@ -185,12 +192,15 @@ def dist_lib():
         _sig(lib, "svdj_dist_comm_init", c_int,
              [c_int, c_int, C.c_char_p, c_double, C.POINTER(c_void_p)])
         _sig(lib, "svdj_dist_comm_destroy", c_int, [c_void_p])
+        _sig(lib, "svdj_dist_id_file", c_int, [c_int, C.c_char_p, c_double, c_void_p, c_size_t])
         _sig(lib, "svdj_dist_geometry", c_int,
              [c_int, c_int, c_int, c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
         _sig(lib, "svdj_dist_choose_block", c_int, [c_int, c_int, c_int, c_int])
         _sig(lib, "svdj_dist_initial_held", c_int, [c_int, c_int, c_i32_p])
         _sig(lib, "svdj_dist_solve", c_int, [C.POINTER(DistProblem), c_void_p])
         _sig(lib, "svdj_dist_storage_cols", c_int, [c_int, c_int])
+        _sig(lib, "svdj_dist_merged_lists", c_int,
+             [c_int, c_int, c_int, c_i32_p, c_int, c_i32_p, c_int, c_i32_p])
         _sig(lib, "svdj_dist_handle_create", c_int, [C.POINTER(DistProblem), C.POINTER(c_void_p)])
         _sig(lib, "svdj_dist_handle_destroy", c_int, [c_void_p])
         _sig(lib, "svdj_dist_last_error", C.c_char_p, [])

@@ -153,14 +153,24 @@ class Communicator:
         ops += [dist.P2POp(dist.irecv, t, s) for t, s in recvs if s != self.rank]
         return ops
 
+    def _host_sync(self):
+        """gloo on device tensors (the one-GPU rehearsal of the multi-rank
+        path) reads and writes them outside stream order: the data must be
+        complete before a call and the result before its first use.  RCCL
+        (stream-ordered) needs none of this."""
+        if self.device.type == "cuda" and not self.async_device:
+            torch.cuda.synchronize(self.device)
+
     def sendrecv(self, sends: list, recvs: list):
         """Grouped point-to-point: sends = [(tensor, dst)], recvs = [(tensor, src)]."""
         if not self.distributed:
             raise RuntimeError("sendrecv on a single rank")
         ops = self._ops(sends, recvs)
         if ops:
+            self._host_sync()
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+            self._host_sync()
 
     def isendrecv(self, sends: list, recvs: list) -> list:
         """Like :meth:`sendrecv` but returns the works without waiting: on the
@@ -203,7 +213,20 @@ class Communicator:
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over ranks (device tensors: RCCL, stream-ordered)."""
         if self.distributed:
+            self._host_sync()
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            self._host_sync()
+        return t
+
+    def ordered_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks added in rank order, t_0 + t_1 + ..., on
+        every rank (all-gather, then local adds): bitwise the same result on
+        any backend and ring, unlike a floating all-reduce."""
+        if self.distributed:
+            parts = self.allgather(t)
+            t.copy_(parts[0])
+            for h in range(1, self.world):
+                t.add_(parts[h])
         return t
 
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
@@ -211,7 +234,9 @@ class Communicator:
         flat = t.contiguous().reshape(-1)
         out = torch.empty(self.world * flat.numel(), dtype=t.dtype, device=t.device)
         if self.distributed:
+            self._host_sync()
             dist.all_gather_into_tensor(out, flat)
+            self._host_sync()
         else:
             out.copy_(flat)
         return out.view((self.world,) + tuple(t.shape))
@@ -225,7 +250,9 @@ class Communicator:
 
     def broadcast(self, t: torch.Tensor, src: int = 0):
         if self.distributed:
+            self._host_sync()
             dist.broadcast(t, src)
+            self._host_sync()
         return t
 
     def max_over_ranks(self, x: float) -> float:

@@ -98,7 +98,17 @@ def quad_round_robin(nb: int) -> np.ndarray:
     """(nb-1, nb//2, 2) block pairs covering every pair of nb blocks once,
     nb % 4 == 0: step 0 pairs the two blocks of every super-block (2i, 2i+1)
     (the full-Gram step of a sweep), then a round robin over the nb/2
-    super-blocks, each super-step as the two steps of a quad."""
+    super-blocks, each super-step as the two steps of a quad (native:
+    svdj_quad_round_robin)."""
+    if nb < 4 or nb % 4:
+        raise ValueError(f"quad_round_robin needs a multiple of 4 blocks, got {nb}")
+    out = _i32((nb - 1, nb // 2, 2))
+    cpu_lib().svdj_quad_round_robin(nb, _ptr(out))
+    return out
+
+
+def quad_round_robin_py(nb: int) -> np.ndarray:
+    """Pure-Python twin of :func:`quad_round_robin`."""
     if nb < 4 or nb % 4:
         raise ValueError(f"quad_round_robin needs a multiple of 4 blocks, got {nb}")
     K = nb // 2
@@ -124,6 +134,18 @@ def quad_bipartite(xs, ys) -> np.ndarray:
     """(h, h, 2) cross pairs between block lists xs and ys (h = len, even)
     in quad order: super-step t pairs super-block (xs[2i], xs[2i+1]) with
     (ys[2j], ys[2j+1]), j = (i + t) mod h/2."""
+    h = len(xs)
+    if h < 2 or h % 2 or len(ys) != h:
+        raise ValueError(f"quad_bipartite needs two even lists of equal length, got {h}, {len(ys)}")
+    out = _i32((h, h, 2))
+    x = np.ascontiguousarray(np.asarray(xs, dtype=np.int32))
+    y = np.ascontiguousarray(np.asarray(ys, dtype=np.int32))
+    cpu_lib().svdj_quad_bipartite(h, _ptr(x), _ptr(y), _ptr(out))
+    return out
+
+
+def quad_bipartite_py(xs, ys) -> np.ndarray:
+    """Pure-Python twin of :func:`quad_bipartite`."""
     h = len(xs)
     if h < 2 or h % 2 or len(ys) != h:
         raise ValueError(f"quad_bipartite needs two even lists of equal length, got {h}, {len(ys)}")

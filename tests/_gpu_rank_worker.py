@@ -6,7 +6,8 @@ or gloo, host-synchronised).  Solves one fixed matrix with the pipelined
 distributed solver and writes rank 0's gathered (U, S, V) plus run info to
 the output file, so runs over different backends can be compared bitwise.
 
-argv: n W chains mode(otf|root|qr) out.pt
+argv: n W chains mode(otf|root|qr|qrbf16) out.pt   (qrbf16: tall bf16 input, the bf16
+problem mode -- BASELINE config 4's kind of job)
 """
 import json
 import os
@@ -30,14 +31,18 @@ def main():
                             exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"))
     solver = DistributedBlockJacobi(cfg, comm)
     g = torch.Generator(device=dev).manual_seed(5)
-    m = 4 * n if mode == "qr" else n
-    if mode == "qr":  # tall: row-distributed CholeskyQR2 + Jacobi on R
+    m = 4 * n if mode in ("qr", "qrbf16") else n
+    if mode in ("qr", "qrbf16"):  # tall: row-distributed CholeskyQR2 + Jacobi on R
         cfg.precondition = "qr"
     A = torch.rand(m, n, generator=g, device=dev, dtype=torch.float32)
+    pdtype = torch.float32
+    if mode == "qrbf16":  # bf16 data, fp32 master copies, bf16 matrix cores
+        A = A.to(torch.bfloat16)
+        pdtype = cfg.dtype = torch.bfloat16
     if mode == "root":
         res = solver.solve(A if comm.rank == 0 else None, gather=True)
     else:
-        res = solver.solve(None, m=m, n=n, dtype=torch.float32,
+        res = solver.solve(None, m=m, n=n, dtype=pdtype,
                            generator=lambda c0, c1: A[:, c0:c1], gather=True)
     if comm.rank == 0:
         torch.save({"U": res.U.cpu(), "S": res.S.cpu(), "V": res.V.cpu(), "A": A.cpu(),

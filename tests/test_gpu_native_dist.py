@@ -8,6 +8,7 @@ ncclSend/ncclRecv exchanges and the all-reduced stop test are the ones an
 orthogonality in fp64 on rank 0 after gathering every rank's columns
 (reference main.cu:1630-1660 computes the same residual)."""
 import os
+import re
 import subprocess
 
 import pytest
@@ -44,7 +45,7 @@ def test_native_dist_launcher(np_, n, dtype, extra):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "SVD MPI+OMP time with U,V calculation" in out
-    assert "converged: 1" in out, out
+    assert re.search(r"converged: [12]\b", out), out
     rel = _value(out, "||A-USVt||_F/||A||_F:")
     ou = _value(out, "||U^TU-I||_F:")
     ov = _value(out, "||V^TV-I||_F:")
@@ -90,7 +91,7 @@ def test_native_persistent_handle_repeat_solves():
                         "--timeout", "120"], capture_output=True, text=True, timeout=170)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
-    assert "converged: 1" in out and "exposed_comm_ms:" in out, out
+    assert re.search(r"converged: [12]\b", out) and "exposed_comm_ms:" in out, out
     assert _value(out, "||A-USVt||_F/||A||_F:") < 2e-5, out
 
 
@@ -103,7 +104,7 @@ def test_native_dist_reference_triangular_input_converges():
                        timeout=170)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
-    assert "converged: 1" in out, out
+    assert re.search(r"converged: [12]\b", out), out
     assert _value(out, "||A-USVt||_F/||A||_F:") < 1e-12, out
     assert _value(out, "||V^TV-I||_F:") < 1e-9, out
 
@@ -119,8 +120,56 @@ def test_native_spread_exchange_matches_direct():
                             "--input", "dense", "--verify", "--exchange", ex, "--timeout", "120"],
                            capture_output=True, text=True, timeout=170)
         out = r.stdout + r.stderr
-        assert r.returncode == 0 and "converged: 1" in out, out[-4000:]
+        assert r.returncode == 0 and re.search(r"converged: [12]\b", out), out[-4000:]
         outs[ex] = out
     for key in ("sweeps:", "||A-USVt||_F:", "||U^TU-I||_F:", "||V^TV-I||_F:"):
         assert outs["direct"].split(key)[1].split("\n")[0] == \
             outs["spread"].split(key)[1].split("\n")[0], key
+
+
+def test_native_auto_exchange_is_measured():
+    """Native engine, 4 RCCL ranks, exchange left on auto: the handle times
+    one direct and one spread half exchange (max over ranks) and keeps the
+    faster; the solve then matches an explicitly direct run to the printed
+    digits (both exchanges deliver the same bits)."""
+    outs = {}
+    for ex in ("auto", "direct"):
+        r = subprocess.run([_exe(), "1024", "--np", "4", "--shared-gpu", "--dtype", "f32",
+                            "--input", "dense", "--verify", "--exchange", ex, "--timeout", "120"],
+                           capture_output=True, text=True, timeout=170)
+        out = r.stdout + r.stderr
+        assert r.returncode == 0 and re.search(r"converged: [12]\b", out), out[-4000:]
+        outs[ex] = out
+    m = re.search(r"exchange calibration: direct ([\d.]+) ms, spread ([\d.]+) ms", outs["auto"])
+    assert m, outs["auto"][-3000:]
+    d, s = float(m.group(1)), float(m.group(2))
+    chosen = re.search(r"exchange: (\w+)", outs["auto"]).group(1)
+    assert chosen == ("spread" if s < 0.9 * d else "direct"), (d, s, chosen)
+    for key in ("sweeps:", "||A-USVt||_F:", "||V^TV-I||_F:"):
+        assert outs["auto"].split(key)[1].split("\n")[0] == \
+            outs["direct"].split(key)[1].split("\n")[0], key
+
+
+def test_native_engine_production_default_matches_python(tmp_path):
+    """The headline configuration (16384^2 fp32, one GPU) in both engines:
+    the native engine takes the same one-GPU issue as the Python executor --
+    merged 128-pair launches of quad steps -- and the same stop rule, so
+    both stop after the same sweep with the same accuracy."""
+    import json
+    import sys
+    out = {}
+    for eng in ("native", "python"):
+        js = tmp_path / f"{eng}.json"
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--engine", eng,
+                            "--steps", "1", "--warmup", "1", "--json-out", str(js)],
+                           capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, MASTER_PORT=str(29960 + len(out))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[eng] = json.loads(js.read_text())
+    nat, py = out["native"], out["python"]
+    for d in (nat, py):
+        assert d["config"]["quad_steps"] and d["config"]["merged_chains"], d["config"]
+        assert d["converged"] and d["accuracy"]["residual_rel"] < 3e-5, d["accuracy"]
+    assert nat["sweeps"] == py["sweeps"], (nat["sweeps"], py["sweeps"])
+    assert abs(nat["accuracy"]["residual_rel"] - py["accuracy"]["residual_rel"]) < 1e-8
+    assert nat["ms_per_step"] < 1.1 * py["ms_per_step"], (nat["ms_per_step"], py["ms_per_step"])

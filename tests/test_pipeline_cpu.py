@@ -1,5 +1,8 @@
 """Half-block pipelined sweep plan (parallel/pipeline.py): coverage and
 exchange structure on CPU."""
+import os
+from pathlib import Path
+
 import pytest
 
 import svdj
@@ -147,7 +150,8 @@ def test_dist_lib_resolves_to_shared_object():
     assert built == b.DIST_LIB and built.suffix == ".so"
     assert b.DIST_DRIVER_BIN.exists() and b.DIST_DRIVER_BIN != built
     path = nat.dist_lib_path()
-    assert path == b.DIST_LIB and path.name == "libsvdj_dist.so"
+    want = Path(os.environ["SVDJ_DIST_LIB"]) if os.environ.get("SVDJ_DIST_LIB") else b.DIST_LIB
+    assert path == want and path.name == "libsvdj_dist.so"  # (the ASan run overrides)
     lib = nat.dist_lib()  # the exact loader bench.py --engine native uses
     assert hasattr(lib, "svdj_dist_solve") and hasattr(lib, "svdj_dist_comm_init")
 
@@ -253,3 +257,87 @@ def test_quad_plan_meets_every_pair_once(P, k):
 def test_quad_plan_needs_multiple_of_4():
     with pytest.raises(ValueError):
         pipeline.sweep_plan(1, 6, schedule.tournament(1).xslot[:, 0], quad=True)
+
+
+def test_dist_id_file_handshake(tmp_path, monkeypatch):
+    """Host part of the native engine's RCCL bootstrap (svdj_dist_id_file,
+    ADVICE r4): a rank accepts only a FRESH id file carrying ITS job token --
+    SVDJ_JOB_TOKEN, or torchrun's run id joined with the restart count, so an
+    elastic restart (or a reused --rdzv-id after a crash) never picks up the
+    dead attempt's id."""
+    import ctypes
+    import os
+    import time
+
+    from svdj.ops import _native as nat
+
+    lib = nat.dist_lib()
+    path = str(tmp_path / "job.id").encode()
+    blob = bytes(range(128))  # sizeof(ncclUniqueId)
+
+    def publish():
+        b = ctypes.create_string_buffer(blob, 128)
+        assert lib.svdj_dist_id_file(0, path, 5.0, b, 128) == 0
+
+    def read(timeout=5.0):
+        b = ctypes.create_string_buffer(128)
+        rc = lib.svdj_dist_id_file(1, path, timeout, b, 128)
+        return rc, b.raw
+
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    monkeypatch.setenv("SVDJ_JOB_TOKEN", "job-a")
+    publish()
+    assert read() == (0, blob)
+    monkeypatch.setenv("SVDJ_JOB_TOKEN", "job-b")  # another job's file: refused
+    assert read(timeout=0.3)[0] == -2
+    # torchrun: same run id, another restart attempt -> refused; same attempt -> read
+    monkeypatch.delenv("SVDJ_JOB_TOKEN")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "rdzv-1")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    publish()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert read(timeout=0.3)[0] == -2
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    assert read() == (0, blob)
+    # a leftover older than the window is refused even with the right token
+    old = time.time() - 3600
+    os.utime(path.decode(), (old, old))
+    assert read(timeout=0.3)[0] == -2
+    assert lib.svdj_dist_id_file(1, path, 0.3, ctypes.create_string_buffer(64), 64) == -2  # size
+
+
+@pytest.mark.parametrize("k,quad", [(8, False), (8, True), (16, True), (128, True)])
+def test_native_merged_lists_match_python(k, quad):
+    """One GPU: the native engine's merged launches (svdj_dist_merged_lists)
+    carry the pair lists and step modes of PipelineExecutor.run_merged --
+    the two parallel tasks of each issue group side by side, step by step --
+    in plain and in quad order (k = 128: the 16384^2 headline's plan)."""
+    import ctypes
+
+    import numpy as np
+
+    from svdj.ops import _native as nat
+
+    lib = nat.dist_lib()
+    plan = pipeline.sweep_plan(1, k, schedule.tournament(1).xslot[:, 0], quad=quad)
+    want_pairs, want_modes, want_meta = [], [], []
+    for it in pipeline.issue_groups(plan.items, True):
+        if not isinstance(it, tuple):
+            continue
+        a, b_ = it
+        assert list(a.modes) == list(b_.modes) and a.pairs.shape == b_.pairs.shape
+        want_meta += [sum(p.size for p in want_pairs), a.pairs.shape[0], 2 * a.pairs.shape[1]]
+        want_pairs.append(np.concatenate([a.pairs, b_.pairs], axis=1).ravel())
+        want_modes += list(a.modes)
+    assert len(want_meta) == 9  # rr0 + rr1, T00 + T11, T01 + T10
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    pairs = np.zeros(4 * k * k, np.int32)
+    modes = np.zeros(4 * k, np.int32)
+    meta = np.zeros(9, np.int32)
+    n = lib.svdj_dist_merged_lists(k, int(quad), 0, pairs.ctypes.data_as(i32p), pairs.size,
+                                   modes.ctypes.data_as(i32p), modes.size, meta.ctypes.data_as(i32p))
+    want = np.concatenate(want_pairs)
+    assert n == want.size
+    assert np.array_equal(pairs[:n], want)
+    assert modes[:len(want_modes)].tolist() == want_modes
+    assert meta.tolist() == want_meta

@@ -523,6 +523,18 @@ def test_quad_bipartite_covers_once(h):
     assert {(a, b) for st in pr for a, b in st.tolist()} == {(x, y) for x in xs for y in ys}
 
 
+@pytest.mark.parametrize("nb", [4, 8, 12, 64, 256])
+def test_quad_round_robin_native_equals_python(nb):
+    assert np.array_equal(S.quad_round_robin(nb), S.quad_round_robin_py(nb))
+
+
+@pytest.mark.parametrize("h", [2, 4, 8, 64])
+def test_quad_bipartite_native_equals_python(h):
+    xs = list(range(3, 3 + h))
+    ys = list(range(100, 100 + 2 * h, 2))
+    assert np.array_equal(S.quad_bipartite(xs, ys), S.quad_bipartite_py(xs, ys))
+
+
 def test_check_quad_steps_rejects_wrong_orientation():
     pr = S.quad_round_robin(8)
     bad = pr.copy()
