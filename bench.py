@@ -414,7 +414,6 @@ def run_native(a, dtype, work):
     p.inner_order = {"cyclic": 0, "bipartite": 1, "cross": 2, "auto": 3}[a.inner_order]
     p.stream_a, p.stream_b, p.stream_comm = sa.cuda_stream, sb.cuda_stream, sc.cuda_stream
     p.hist = C.cast(hist, C.POINTER(C.c_double))
-    p.stagger = 1 if a.stagger else 0
     p.exchange = {"auto": 0, "direct": 1, "spread": 2}[a.exchange]
     p.timeout_s = float(timeout)
     p.comm_timing = 1 if a.comm_timing else 0
@@ -496,7 +495,7 @@ def run_native(a, dtype, work):
                        "inner_order": {0: "cyclic", 1: "bipartite", 2: "cross"}.get(
                            int(p.inner_order_used), a.inner_order),
                        "exchange": {1: "direct", 2: "spread"}.get(int(p.exchange_used), "direct"),
-                       "staggered": bool(a.stagger), "root_owned": False,
+                       "root_owned": False,
                        "quad_steps": bool(p.quad_used), "merged_chains": bool(p.merged_used),
                        "stop_rule": a.stop_rule},
             "sweeps": sweeps, "converged": conv, "stop_reason": sorted(reasons),
@@ -557,10 +556,6 @@ def main():
     p.add_argument("--inner-order", default=svdj_default_inner(),
                    choices=["auto", "cyclic", "bipartite", "cross"],
                    help="EVD ordering of the block cross steps")
-    p.add_argument("--stagger", dest="stagger", action="store_true", default=None,
-                   help="offset the two step chains by an EVD (svdj_block_steps2)")
-    p.add_argument("--no-stagger", dest="stagger", action="store_false",
-                   help="issue the two step chains independently (the default)")
     p.add_argument("--mma", default="auto", choices=["auto", "native", "bf16x6", "bf16x3"],
                    help="block apply matrix cores (auto = bf16x6 for fp32 W=64 steps, f32/f64 "
                         "MFMA otherwise; bf16x6 = 3-way bf16 split at fp32 accuracy, bf16x3 = "
@@ -608,7 +603,7 @@ def main():
     work = torch.float64 if dtype == torch.float64 else torch.float32
     cfg = svdj.SolverConfig(dtype=dtype, block=a.block, max_sweeps=a.max_sweeps, tol=a.tol,
                             max_inner_sweeps=a.inner, chains=a.chains, mma=a.mma,
-                            stagger=bool(a.stagger), precondition=a.precondition,
+                            precondition=a.precondition,
                             inner_order=a.inner_order,
                             progress=a.progress, comm_timing=a.comm_timing, exchange=a.exchange,
                             quad=a.quad, stop_rule=a.stop_rule)
@@ -725,7 +720,6 @@ def main():
                 "precondition": last.info.get("precondition", "none"),
                 "chains": a.chains,
                 "inner_order": last.info.get("inner_order", a.inner_order),
-                "staggered": bool(a.stagger),
                 "root_owned": a.root_owned,
                 "exchange": last.info.get("exchange", a.exchange),
                 "quad_steps": bool(last.info.get("quad", False)),

@@ -63,11 +63,6 @@ class SolverConfig:
     # + Jacobi on R + U = Q U_R 1.99 s (Householder QR via rocSOLVER geqrf: 5.4 s).
     qr_ratio: float = 2.0
     chains: int = 2                 # block path: independent step chains on separate streams
-    # offset the two chains by an EVD (svdj_block_steps2).  Off: since the
-    # bipartite EVD and the apply geometry of round 2, issuing the chains
-    # independently is faster (8-GPU rank plan 59.4 -> 57.5 ms per sweep, 1 GPU
-    # 16384^2 5.79 -> 5.73 s, profiles/r2_stag); round 1 needed the offset
-    stagger: bool = False
     num_threads: int = 0            # CPU oracle OpenMP threads (0: default)
     progress: bool = False          # rank 0 prints one line per sweep to stderr
     comm_timing: bool = False       # distributed: HIP-event timing of every exchange

@@ -9,8 +9,8 @@
 //   round 0 : round robin inside each slot            (chain 0: slot 0, 1: slot 1)
 //   round r : I0xS0 (0), I0xS1 (0), I1xS0 (1), send half 0 of the slot
 //             replaced next, I1xS1 (1), send half 1   (last round: no sends)
-// Tasks on different chains touching disjoint halves are issued as one
-// staggered svdj_block_steps2 pair; every dependency (half -> task, task ->
+// Tasks on different chains touching disjoint halves form one issue group
+// (one GPU: merged into single launches); every dependency (half -> task, task ->
 // send, arrival -> consumer) is a HIP event, so exchanges overlap the compute
 // of the other halves (reference main.cu:582-680, 854-936 sends whole blocks
 // with blocking MPI between rounds).  The stop test is an RCCL all-reduce (max
@@ -1092,22 +1092,12 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         const int ba = L.loc[t.hv[0] / 2][t.hv[0] % 2], bb = L.loc[t.hv[1] / 2][t.hv[1] % 2];
         return t.dev[ba][bb];
       };
-      if (n_t == 2 && p->stagger) {
-        const TItem &x = titems[gr.a], &y = titems[gr.b];
-        const int cx = x.stream, cy = y.stream;
-        SVDJC(svdj_block_steps2(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
-                                dev_pairs(x), x.t->npairs, x.t->steps, x.t->modes.data(), h->ws[cx],
-                                h->wsb, st[cx], dev_pairs(y), y.t->npairs, y.t->steps,
-                                y.t->modes.data(), h->ws[cy], h->wsb, st[cy], p->tol, p->tol_mode,
-                                1, h->metric, p->mma));
-      } else {
-        for (int q = 0; q < n_t; ++q) {  // one chain, or two issued independently
-          const TItem& z = titems[idx[q]];
-          const int cz = z.stream;
-          SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
-                                 dev_pairs(z), z.t->npairs, z.t->steps, z.t->modes.data(), p->tol,
-                                 p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, p->mma, st[cz]));
-        }
+      for (int q = 0; q < n_t; ++q) {  // one chain, or two issued independently
+        const TItem& z = titems[idx[q]];
+        const int cz = z.stream;
+        SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
+                               dev_pairs(z), z.t->npairs, z.t->steps, z.t->modes.data(), p->tol,
+                               p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, p->mma, st[cz]));
       }
       for (int q = 0; q < n_t; ++q) {
         const Item& x = items[idx[q]];

@@ -28,7 +28,6 @@
 
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -2372,11 +2371,18 @@ struct Geometry {
 // by evd_cross_kernel / quad_update_kernel); the apply is a persistent grid.
 static void quad_geometry(Geometry& g, int P, int m_pad, int n_v) {
   // gram_quad_kernel: one workgroup (160 KB LDS, one per CU) per quad and row
-  // chunk, ~256 of them; from 32 quads per launch every quad keeps 8 chunks,
+  // chunk, ~256 of them; from 32 quads per launch every quad keeps 4 chunks,
   // so a merged one-GPU launch (two chains' quads in one) sums every Gram
-  // exactly as the two chains do (bitwise the same solve, as make_geometry)
+  // exactly as the two chains do (bitwise the same solve, as make_geometry).
+  // 64 quads (16384^2 merged), us per quad step: 2 chunks 963-979, 4 chunks
+  // 874-884, 8 chunks 933 (profiles/r5_gram)
   const int nq = P / 2 > 0 ? P / 2 : 1;
-  const int want = nq >= 32 ? 8 : (256 + nq - 1) / nq;
+  int want = nq >= 32 ? 4 : (256 + nq - 1) / nq;
+  static const int forced = [] {  // A/B measurements only
+    const char* e = getenv("SVDJ_QUAD_GRAM_CHUNKS");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) want = forced;
   const int maxc = m_pad / 128;
   g.qgch = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.qgrows = round_up((m_pad + g.qgch - 1) / g.qgch, 128);
@@ -2395,10 +2401,17 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // Steps of >= 64 pairs keep the 64-pair chunking (4 row chunks): a merged
   // one-GPU step (two chains' 64-pair steps in one launch, pipeline.py
   // run_merged) then sums every pair's Gram exactly as the two chains do, so
-  // the solve is bitwise the two-chain one (same sweeps).
+  // the solve is bitwise the two-chain one (same sweeps).  Measured at 128
+  // pairs (16384^2 merged, quad off): 4 chunks 4.70 s vs 2 chunks (the
+  // target rule) 4.73 s, residual 1.37e-5 vs 1.52e-5 (profiles/r5_gram).
   const int gram_target = P >= 32 ? 256 : 512;
   int want = (gram_target + P - 1) / P;
   if (P >= 64 && want < 4) want = 4;
+  static const int forced = [] {  // A/B measurements only
+    const char* e = getenv("SVDJ_GRAM_CHUNKS");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) want = forced;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
   g.grows = round_up((m_pad + g.gchunks - 1) / g.gchunks, 128);
@@ -2752,80 +2765,6 @@ static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inn
   return 0;
 }
 
-// Recycled cross-stream events of the staggered two-chain issue.  One ring per
-// (recording stream, waiting stream) pair, created on the device the streams
-// belong to (not the caller's current device) and looked up under a mutex, so
-// solvers on several devices or host threads never share an event.  A wait
-// captures the event's state when it is enqueued, so an event can be
-// re-recorded once its waits are issued -- within ONE stream pair, whose
-// issue order the caller serialises.
-static hipEvent_t* stagger_events(hipStream_t rec, hipStream_t wait, int& n) {
-  constexpr int kRing = 64;
-  struct Ring {
-    hipStream_t rec, wait;
-    hipEvent_t ev[kRing];
-  };
-  static std::mutex mu;
-  static std::vector<Ring*> rings;
-  std::lock_guard<std::mutex> lock(mu);
-  n = kRing;
-  for (Ring* r : rings)
-    if (r->rec == rec && r->wait == wait) return r->ev;
-  int sdev = 0, cur = 0;
-  if (hipStreamGetDevice(rec, &sdev) != hipSuccess || hipGetDevice(&cur) != hipSuccess)
-    return nullptr;
-  if (sdev != cur && hipSetDevice(sdev) != hipSuccess) return nullptr;
-  Ring* r = new Ring{rec, wait, {}};
-  bool ok = true;
-  for (int i = 0; i < kRing && ok; ++i)
-    ok = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming) == hipSuccess;
-  if (sdev != cur) (void)hipSetDevice(cur);
-  if (!ok) {
-    delete r;  // (events created before the failure are leaked; error path only)
-    return nullptr;
-  }
-  rings.push_back(r);
-  return r->ev;
-}
-
-// Two independent chains on two streams, staggered (SolverConfig.stagger):
-// chain B's step s starts when chain A's EVD of step s has finished, so B's
-// gram/EVD run under A's apply and A's next gram/EVD under B's apply.  Round
-// 1 needed this; since the bipartite EVD and the round-2 apply geometry,
-// independent issue (one svdj_block_steps per chain) is faster (8-GPU rank
-// plan 59.4 -> 57.5 ms per sweep), so it is off by default.  A symmetric
-// stagger, four chains in a cascade and hipGraph replay of this issue were
-// measured slower in round 2 and removed (git history, profiles/r2_*).
-template <typename T, int W>
-static int block_steps2_t(const Chain<T>& a, const Chain<T>& b, double tol, int absmode,
-                          int max_inner, uint32_t* metric, int mma) {
-  int ne = 0;
-  hipEvent_t* ev = stagger_events(a.st, b.st, ne);
-  if (!ev) {
-    set_error("stagger events unavailable");
-    return -100;
-  }
-  const int n = a.steps > b.steps ? a.steps : b.steps;
-  for (int s = 0; s < n; ++s) {
-    int rc = 0;
-    if (s < a.steps) {
-      rc = launch_gram_evd<T, W>(a, s, tol, absmode, max_inner, metric, mma);
-      if (!rc && s < b.steps && hipEventRecord(ev[s % ne], a.st) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_apply<T, W>(a, s, mma);
-    }
-    if (!rc && s < b.steps) {
-      if (s < a.steps && hipStreamWaitEvent(b.st, ev[s % ne], 0) != hipSuccess) rc = -100;
-      if (!rc) rc = launch_gram_evd<T, W>(b, s, tol, absmode, max_inner, metric, mma);
-      if (!rc) rc = launch_apply<T, W>(b, s, mma);
-    }
-    if (rc) {
-      if (rc == -100) set_error("stagger event record/wait failed");
-      return rc;
-    }
-  }
-  return 0;
-}
-
 }  // namespace svdj
 
 using namespace svdj;
@@ -2870,31 +2809,19 @@ template <typename T, int W>
 static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv, void* D,
                           const int32_t* pairs, int P, int steps, const int32_t* modes,
                           double tol, int absmode, int max_inner, void* ws, size_t ws_bytes,
-                          uint32_t* metric, int mma, void* stream, const int32_t* pairs2, int P2,
-                          int steps2, const int32_t* modes2, void* ws2, size_t ws2_bytes,
-                          void* stream2) {
-  Chain<T> a, b;
-  int rc = chain_init<T, W>(a, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
+                          uint32_t* metric, int mma, void* stream) {
+  Chain<T> c;
+  int rc = chain_init<T, W>(c, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
                             ws, ws_bytes, mma, (hipStream_t)stream);
   if (rc) return rc;
-  if (!pairs2 || P2 <= 0 || steps2 <= 0)
-    return block_steps_t<T, W>(a, tol, absmode, max_inner, metric, mma);
-  if (ws2 == ws || stream2 == stream) {
-    set_error("staggered chains need distinct workspaces and streams");
-    return -2;
-  }
-  rc = chain_init<T, W>(b, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs2, P2, steps2, modes2,
-                        ws2, ws2_bytes, mma, (hipStream_t)stream2);
-  if (rc) return rc;
-  return block_steps2_t<T, W>(a, b, tol, absmode, max_inner, metric, mma);
+  return block_steps_t<T, W>(c, tol, absmode, max_inner, metric, mma);
 }
 
-static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v, int ldv,
-                     void* D, const int32_t* pairs, int P, int steps, const int32_t* modes,
-                     double tol, int tol_mode, int max_inner, void* ws, size_t ws_bytes,
-                     uint32_t* metric, int mma, void* stream, const int32_t* pairs2, int P2,
-                     int steps2, const int32_t* modes2, void* ws2, size_t ws2_bytes,
-                     void* stream2) {
+extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
+                                int ldv, void* D, const int32_t* pairs, int P, int steps,
+                                const int32_t* modes, double tol, int tol_mode, int max_inner,
+                                void* ws, size_t ws_bytes, uint32_t* metric, int mma,
+                                void* stream) {
   int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
   if (rc) return rc;
   if (tol_mode != 0 && tol_mode != 1) {
@@ -2904,7 +2831,7 @@ static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int
   if (P <= 0 || steps < 0) return 0;
 #define SVDJ_STEPS_ARGS                                                                       \
   m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol, tol_mode, max_inner, ws, ws_bytes, \
-      metric, mma, stream, pairs2, P2, steps2, modes2, ws2, ws2_bytes, stream2
+      metric, mma, stream
   if (dtype == 0 && W == 32) return steps_dispatch<float, 32>(SVDJ_STEPS_ARGS);
   if (dtype == 0 && W == 64) return steps_dispatch<float, 64>(SVDJ_STEPS_ARGS);
   if (dtype == 1 && W == 32) return steps_dispatch<double, 32>(SVDJ_STEPS_ARGS);
@@ -2912,27 +2839,6 @@ static int steps_any(int dtype, int W, int m_pad, void* A, int lda, void* V, int
 #undef SVDJ_STEPS_ARGS
   set_error("unsupported (dtype=%d, W=%d); supported: W in {32, 64}", dtype, W);
   return -3;
-}
-
-extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
-                                int ldv, void* D, const int32_t* pairs, int P, int steps,
-                                const int32_t* modes, double tol, int tol_mode, int max_inner,
-                                void* ws, size_t ws_bytes, uint32_t* metric, int mma,
-                                void* stream) {
-  return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
-                   tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, nullptr, 0, 0, nullptr,
-                   nullptr, 0, nullptr);
-}
-
-extern "C" int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,
-                                 int ldv, void* D, const int32_t* pairs, int P, int steps,
-                                 const int32_t* modes, void* ws, size_t ws_bytes, void* stream,
-                                 const int32_t* pairs2, int P2, int steps2, const int32_t* modes2,
-                                 void* ws2, size_t ws2_bytes, void* stream2, double tol,
-                                 int tol_mode, int max_inner, uint32_t* metric, int mma) {
-  return steps_any(dtype, W, m_pad, A, lda, V, n_v, ldv, D, pairs, P, steps, modes, tol,
-                   tol_mode, max_inner, ws, ws_bytes, metric, mma, stream, pairs2, P2, steps2,
-                   modes2, ws2, ws2_bytes, stream2);
 }
 
 extern "C" int svdj_block_solve(int dtype, int W, int m_pad, void* A, int lda, void* V, int n_v,

@@ -70,8 +70,6 @@ typedef struct {
   int inner_order;            // EVD of the cross steps: 0 cyclic, 1 bipartite (mode 2),
                               // 2 cross-only bipartite (mode 3), 3 auto
                               // (svdj_choose_inner_order of the half super-block pairs)
-  int stagger;                // 1: the two chains of a group offset by an EVD
-                              // (svdj_block_steps2); 0 (default): issued independently
   int exchange;               // half super-block transfer: 0 auto (from 4 ranks both are
                               // timed on the job's links when the handle is created and
                               // spread is kept only if >= 10 % faster, as
@@ -129,7 +127,7 @@ int svdj_dist_handle_destroy(void* handle);
 int svdj_dist_solve(svdj_dist_problem* p, void* sigma);
 
 // Issue order of one sweep on `rank` (host only, for tests): per group 7 ints
-// {kind, ...}: kind 0 = one task {stream, half, half}, 1 = a staggered pair
+// {kind, ...}: kind 0 = one task {stream, half, half}, 1 = a joint pair
 // {stream, half, half, stream, half, half}, 2 = a half exchange {round, slot,
 // half}; halves are slot*2 + half.  Returns the group count (<= cap) or <0.
 int svdj_dist_plan(int world, int rank, int32_t* out, int cap);

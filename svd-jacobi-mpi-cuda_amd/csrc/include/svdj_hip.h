@@ -88,19 +88,6 @@ int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, void* V,
                      int max_inner_sweeps, void* workspace, size_t ws_bytes,
                      uint32_t* metric, int mma, void* stream);
 
-// Two independent chains of steps (disjoint blocks) on two streams with
-// their own workspaces, staggered: step s of chain 2 starts when the EVD of
-// step s of chain 1 has finished, so one chain's Gram/EVD runs under the
-// other's apply instead of both chains running in lockstep.
-int svdj_block_steps2(int dtype, int W, int m_pad, void* A, int lda, void* V,
-                      int n_v, int ldv, void* D, const int32_t* pairs, int P,
-                      int steps, const int32_t* modes, void* workspace,
-                      size_t ws_bytes, void* stream, const int32_t* pairs2,
-                      int P2, int steps2, const int32_t* modes2,
-                      void* workspace2, size_t ws2_bytes, void* stream2,
-                      double tol, int tol_mode, int max_inner_sweeps,
-                      uint32_t* metric, int mma);
-
 // Single-GPU block solve: round-robin over nb = ncols/W blocks (nb even),
 // first step of every sweep in full mode; inner_order 0 = cyclic EVD in every
 // step, 1 = bipartite EVD in the cross steps (mode 2), 2 = cross-only

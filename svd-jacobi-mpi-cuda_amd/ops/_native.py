@@ -117,10 +117,6 @@ def hip_lib():
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
               c_int, c_int, c_i32_p, c_double, c_int, c_int, c_void_p, c_size_t, c_void_p, c_int,
               c_void_p])
-        _sig(lib, "svdj_block_steps2", c_int,
-             [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
-              c_int, c_int, c_i32_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_int,
-              c_i32_p, c_void_p, c_size_t, c_void_p, c_double, c_int, c_int, c_void_p, c_int])
         _sig(lib, "svdj_block_solve", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
               c_double, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_f64_p, c_int,
@@ -148,7 +144,7 @@ class DistProblem(C.Structure):
                 ("W", c_int), ("m_pad", c_int), ("n_v", c_int), ("B", c_int),
                 ("At", c_void_p), ("Vt", c_void_p), ("D", c_void_p), ("held", C.c_int32 * 2),
                 ("tol", c_double), ("tol_mode", c_int), ("max_sweeps", c_int), ("mma", c_int),
-                ("inner_order", c_int), ("stagger", c_int), ("exchange", c_int),
+                ("inner_order", c_int), ("exchange", c_int),
                 ("stream_a", c_void_p),
                 ("stream_b", c_void_p), ("stream_comm", c_void_p), ("timeout_s", c_double),
                 ("comm_timing", c_int), ("fault_rank", c_int), ("fault_sweep", c_int),

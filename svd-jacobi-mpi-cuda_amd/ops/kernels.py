@@ -352,37 +352,6 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
                 metric[4] += stats.get("ncols", 0)
 
 
-def block_steps2(At, Vt, D, m_pad, W, tol, max_inner, metric, chain_a, chain_b, mma="native",
-                 pool: dict | None = None, tol_mode="relative", inner_order="cyclic"):
-    """Two independent chains of block steps, staggered (svdj_block_steps2).
-    ``chain_x = (pairs, modes, ws_slot, stream)``: device pairs (steps, P, 2),
-    host modes, a workspace slot and the torch stream of that chain.  Step s
-    of chain b starts when chain a's EVD of step s is done.  On CPU tensors
-    the chains run one after the other."""
-    if not At.is_cuda:
-        for pairs, modes, slot, _ in (chain_a, chain_b):
-            block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, slot, mma, pool,
-                        tol_mode, inner_order)
-        return
-    _check_layout(At, m_pad)
-    check_block(At.dtype, W)
-    args = []
-    for pairs, modes, slot, stream in (chain_a, chain_b):
-        steps, P = int(pairs.shape[0]), int(pairs.shape[1])
-        kmodes = step_modes(modes, inner_order)
-        ws = block_workspace(At.dtype, W, P, m_pad, At.device, slot, pool,
-                             quad=any(int(x) == 4 for x in kmodes))
-        md = (C.c_int32 * max(steps, 1))(*kmodes)
-        args.append((_ptr(pairs), P, steps, md, _ptr(ws), ws.numel(),
-                     C.c_void_p(stream.cuda_stream)))
-    n_v = Vt.shape[1] if Vt is not None else 0
-    ldv = Vt.stride(0) if Vt is not None else 0
-    hip_check(hip_lib().svdj_block_steps2(
-        dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv, _ptr(D),
-        *args[0], *args[1], float(tol), tol_mode_code(tol_mode), int(max_inner), _ptr(metric),
-        mma_code(mma, At.dtype)), "block_steps2")
-
-
 def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
                rows_per_chunk: int) -> torch.Tensor:
     """Cross Gram A_bi^T A_bj of every (bi, bj) in ``pairs`` (P, 2) on the
@@ -473,7 +442,7 @@ __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric", "set_norm_floor",
     "METRIC_WORDS", "read_stop", "metric_stop_values", "sweep_converged", "STOP_RULES",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
-    "block_workspace", "block_steps", "block_steps2", "block_solve", "check_block", "MMA_CODES", "mma_code",
+    "block_workspace", "block_steps", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",
     "gram_cross", "gram_quad",
 ]

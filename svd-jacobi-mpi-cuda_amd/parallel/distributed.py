@@ -306,14 +306,6 @@ class DistributedBlockJacobi(Solver):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                               inner_order=inner)
-
-            def run_pair(a, b):
-                K.block_steps2(At, Vt, D, m_pad, W, tol, cfg.max_inner_sweeps, metric, a, b,
-                               mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                               inner_order=inner)
-
-            if not cfg.stagger:
-                run_pair = None
         # One rank, no exchanges, >= 64 pairs per chain step: the two chains'
         # parallel tasks merged into single launches of 128+ pairs
         # (PipelineExecutor.run_merged) -- bitwise the two-chain solve (the
@@ -331,8 +323,7 @@ class DistributedBlockJacobi(Solver):
                 if pipelined and merged and not comm.distributed:
                     ex.run_merged(splan, run_steps)
                 elif pipelined:
-                    t_comm += ex.run(splan, run_steps, phys, None if merged else run_pair,
-                                     merge=merged)
+                    t_comm += ex.run(splan, run_steps, phys, merge=merged)
                     held = phys[g]
                 for r in range(0 if not pipelined else tour.rounds, tour.rounds):
                     if r > 0 and P > 1:

@@ -127,10 +127,10 @@ def sweep_plan(P: int, k: int, xslot: np.ndarray, chains: int = 2, quad: bool = 
     return plan
 
 
-def issue_groups(items: list, stagger: bool, max_group: int = 2) -> list:
+def issue_groups(items: list, joint: bool, max_group: int = 2) -> list:
     """The plan's items regrouped for issue: a Task, a Send, or a tuple of up
-    to ``max_group`` tasks issued jointly as staggered chains
-    (ops.kernels.block_steps2).
+    to ``max_group`` independent tasks issued jointly (merged into single
+    launches on one GPU, :meth:`PipelineExecutor.run_merged`).
 
     Greedy: a task is grouped with the following tasks (Sends in between are
     skipped) while each runs on a new stream, touches parts disjoint from the
@@ -143,7 +143,7 @@ def issue_groups(items: list, stagger: bool, max_group: int = 2) -> list:
     i, n = 0, len(items)
     while i < n:
         it = items[i]
-        if not (stagger and isinstance(it, Task)):
+        if not (joint and isinstance(it, Task)):
             out.append(it)
             i += 1
             continue
@@ -486,11 +486,11 @@ class PipelineExecutor:
                 run_steps(self._pairs(index[id(t)], t), t.modes, 0)
         return 0.0
 
-    def run(self, plan: SweepPlan, run_steps, phys, run_pair=None, merge: bool = False) -> float:
+    def run(self, plan: SweepPlan, run_steps, phys, merge: bool = False) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
-        steps on the current stream; ``run_pair(a, b)`` (optional) enqueues two
-        independent chains staggered, ``a``/``b`` = (pairs, modes, slot,
-        stream).  ``phys`` (per-GPU placement of whole super-blocks) is
+        steps on the current stream; ``merge``: the joint task groups as
+        single launches (SVDJ_MERGE_CHAINS=1 with exchanges; measured slower
+        there).  ``phys`` (per-GPU placement of whole super-blocks) is
         updated after both halves of a round arrived.  Returns host seconds
         spent issuing/blocking on exchanges."""
         import time
@@ -511,7 +511,7 @@ class PipelineExecutor:
         index = {id(it): i for i, it in enumerate(plan.items)}
         groups = self._groups.get((id(plan), merge))
         if groups is None:
-            groups = issue_groups(plan.items, run_pair is not None or merge)
+            groups = issue_groups(plan.items, merge)
             self._groups[(id(plan), merge)] = groups
         for it in groups:
             if isinstance(it, Send):
@@ -556,12 +556,8 @@ class PipelineExecutor:
                 done = self._event()
                 done.record(sa)
                 sb.wait_event(done)
-            elif len(tasks) == 2 and run_pair is not None:
-                a, b = tasks
-                run_pair((pairs[0], a.modes, a.stream, self.streams[a.stream]),
-                         (pairs[1], b.modes, b.stream, self.streams[b.stream]))
-            else:  # one task, or a group that cannot merge and has no staggered issue:
-                # each task on its own stream (as run_merged falls back)
+            else:  # one task, or a group that cannot merge: each task on its
+                # own stream (as run_merged falls back)
                 for q, t in enumerate(tasks):
                     with torch.cuda.stream(self.streams[t.stream]):
                         run_steps(pairs[q], t.modes, t.stream)

@@ -327,41 +327,6 @@ def test_svd_end_to_end_bipartite(svdj, cuda, dtype, order):
     assert rep["orth_u_fro"] < ou and rep["orth_v_fro"] < ov, rep
 
 
-def test_block_steps2_staggered_matches_sequential(svdj, cuda):
-    """svdj_block_steps2: two chains on two streams, chain B's step s waiting
-    for chain A's EVD of step s, on disjoint blocks give bitwise the result of
-    running the chains one after the other on one stream."""
-    K = svdj.ops.kernels
-    W, nb, m, m_pad = 32, 8, 700, 768
-    n = nb * W
-    A0 = _rand_At(n, m_pad, m, torch.float32, cuda, seed=11)
-    rr = svdj.parallel.schedule.round_robin(4)  # 3 steps x 2 pairs on 4 blocks
-    streams = [torch.cuda.Stream(cuda) for _ in range(2)]
-    chains = [(torch.from_numpy(rr + 4 * c).to(cuda), [1, 0, 0], c, streams[c]) for c in range(2)]
-
-    def run(staggered):
-        At = A0.clone()
-        Vt = torch.zeros(n, n, dtype=torch.float32, device=cuda)
-        K.set_identity(Vt, n)
-        D = K.col_norms2(At, m_pad)
-        metric = K.new_metric(cuda)
-        torch.cuda.synchronize()
-        if staggered:
-            K.block_steps2(At, Vt, D, m_pad, W, 1e-6, 1, metric, chains[0], chains[1], pool={},
-                           inner_order="bipartite")
-        else:
-            for pairs, modes, slot, _ in chains:
-                K.block_steps(At, Vt, D, m_pad, pairs, W, modes, 1e-6, 1, metric, slot, pool={},
-                              inner_order="bipartite")
-        torch.cuda.synchronize()
-        return At, Vt, D, K.read_metric(metric)
-
-    a1, v1, d1, m1 = run(True)
-    a0, v0, d0, m0 = run(False)
-    assert m1[1] == m0[1] > 0
-    assert torch.equal(a1, a0) and torch.equal(v1, v0) and torch.equal(d1, d0)
-
-
 @pytest.mark.parametrize("W", [32, 64])
 @pytest.mark.parametrize("m,m_pad,rows", [(100, 128, 128), (500, 512, 128), (4000, 4096, 1024),
                                           (5000, 5120, 3072), (3000, 3072, 256)])

@@ -45,8 +45,9 @@ def test_odd_k_rejected():
 
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("k", [2, 4, 6])
-def test_stagger_groups_keep_coverage(P, k):
-    """Joint (staggered) issue pairs independent tasks of different streams;
+def test_joint_groups_keep_coverage(P, k):
+    """Joint issue (the merged one-GPU launches) pairs independent tasks of
+    different streams;
     the regrouped order (Sends moved after a pair) still meets every pair
     once and never moves a Send past a task that touches its half."""
     tour = schedule.tournament(P)

@@ -5,7 +5,7 @@ Splits the span of the last solve in a rocprofv3 --kernel-trace SQLite database
 during which (a) an apply or Gram kernel is running (the chip is doing the
 wide, GPU-filling work), (b) only EVD kernels run (one workgroup per pair:
 the chip is mostly idle), (c) nothing of ours runs.  (b)+(c) is the latency
-the two staggered chains fail to hide.
+the two overlapped chains fail to hide.
 
     python tools/trace_crit.py run_results.db [more.db ...]
 """
