@@ -1990,15 +1990,31 @@ __global__ __launch_bounds__(kUpdThreads) void quad_update_kernel(
     Ls[r * (W + 4) + cc] = (float)Lg[(size_t)r * N + cc];
   }
   // slabs of quad q: r = 0 (a,d), 1 (b,c), 2 (a,b), 3 (c,d), gch chunks each
-  const float* base = slabs + (size_t)q * 4 * gch * W * W;
-  for (int idx = tid; idx < 4 * W * W; idx += kUpdThreads) {
-    const int r = idx / (W * W), e = idx % (W * W), i = e / W, jj = e % W;
-    const float* p = base + (size_t)r * gch * W * W + e;
-    double s = 0.0;
-    for (int k = 0; k < gch; ++k) s += (double)p[(size_t)k * W * W];
-    const int row = r == 0 ? i : r == 1 ? W + jj : r == 2 ? i : W + i;
-    const int col = r == 0 ? W + jj : r == 1 ? i : r == 2 ? jj : W + jj;
-    Ms[row * MP + col] = (float)s;
+  // (16-byte loads, four independent sums per thread and four slabs' worth in
+  // flight: the one-float loop was load-latency bound, 94 us per 128-pair quad
+  // step at 83 % wait-any, profiles/r5_prof)
+  const float4* base = reinterpret_cast<const float4*>(slabs + (size_t)q * 4 * gch * W * W);
+  constexpr int E4 = W * W / 4;
+#pragma unroll 4
+  for (int idx = tid; idx < 4 * E4; idx += kUpdThreads) {
+    const int r = idx / E4, e4 = idx % E4, i = (4 * e4) / W, jj = (4 * e4) % W;
+    const float4* p = base + (size_t)r * gch * E4 + e4;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int k = 0; k < gch; ++k) {
+      const float4 v = p[(size_t)k * E4];
+      s0 += (double)v.x;
+      s1 += (double)v.y;
+      s2 += (double)v.z;
+      s3 += (double)v.w;
+    }
+    const double sv[4] = {s0, s1, s2, s3};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ju = jj + u;
+      const int row = r == 0 ? i : r == 1 ? W + ju : r == 2 ? i : W + i;
+      const int col = r == 0 ? W + ju : r == 1 ? i : r == 2 ? ju : W + ju;
+      Ms[row * MP + col] = (float)sv[u];
+    }
   }
   __syncthreads();
   const int li = lane & 31, lk = lane >> 5;
@@ -2286,12 +2302,17 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   const float* own = A + (size_t)__builtin_amdgcn_readfirstlane(blk(wave >> 1) * W + (wave & 1) * 32) * lda;
   // products in [a b c d] block order: (x, y) and the slab each goes to
   constexpr int PX[6] = {0, 1, 0, 1, 0, 2}, PY[6] = {2, 3, 3, 2, 1, 3};  // ac bd ad bc ab cd
+  // raw image [col][16-byte row chunk], chunk slot j of column col holding
+  // rows 4 (j ^ (col & 7)) .. + 3: the split's reads (8 rows of one column per
+  // lane, lanes at a 128-byte column stride) then spread over all banks
+  // instead of piling onto a few (35 % bank-conflict cycles unswizzled)
   auto dma = [&](int sl, int buf) {
     const int r0 = r_begin + 32 * sl;
     char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
+    const int jr = ((lane & 7) ^ (lane >> 3)) * 4;  // col & 7 == lane >> 3 for every i
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds(own + (size_t)(8 * i + (lane >> 3)) * lda + r0 + (lane & 7) * 4,
+      __builtin_amdgcn_global_load_lds(own + (size_t)(8 * i + (lane >> 3)) * lda + r0 + jr,
                                        dst + i * 1024, 16, 0, 0);
   };
   f32x16 acc[3], lo[3];
@@ -2306,8 +2327,9 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
       bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(R + c * 32 + 16 * kk + 8 * h);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(R + c * 32 + 16 * kk + 8 * h + 4);
+        const int rc = 4 * kk + 2 * h;  // row chunks rc, rc + 1 of column c
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * (rc ^ (c & 7)));
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * ((rc + 1) ^ (c & 7)));
         bf16x8 parts[NP];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
