@@ -1885,12 +1885,12 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 // output fp32).  Same row-parallel rotation loop as qbuild_kernel; a skipped
 // pair contributes the identity (phase 1 writes it: T1 is read by update and
 // phase 2 even when its pair did not rotate).
-template <int PHASE, int R>
-__global__ __launch_bounds__(kQbThreads) void qbuild_quad_kernel(
+template <int PHASE, int R, int NT>
+__global__ __launch_bounds__(NT) void qbuild_quad_kernel(
     const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
     const int32_t* __restrict__ skip, double* __restrict__ T1, float* __restrict__ Tq) {
   constexpr int W = 64, N = 2 * W, QN = 4 * W;
-  constexpr int WAVES = kQbThreads / SVDJ_WAVE;
+  constexpr int WAVES = NT / SVDJ_WAVE;
   static_assert((PHASE == 1 ? N : QN) % (R * WAVES) == 0, "row cover");
   using Q2 = Pair2<double>;
   __shared__ Q2 rs[kQbChunk * W];
@@ -1924,7 +1924,7 @@ __global__ __launch_bounds__(kQbThreads) void qbuild_quad_kernel(
   }
   for (int t0 = 0; t0 < ns; t0 += kQbChunk) {
     const int nc = ns - t0 < kQbChunk ? ns - t0 : kQbChunk;
-    for (int i = threadIdx.x; i < nc * W; i += kQbThreads) rs[i] = rp[(size_t)t0 * W + i];
+    for (int i = threadIdx.x; i < nc * W; i += NT) rs[i] = rp[(size_t)t0 * W + i];
     __syncthreads();
     Q2 n0 = rs[a], n1 = nc > 1 ? rs[W + a] : Q2{1.0, 0.0};
     for (int t = 0; t < nc; ++t) {
@@ -2611,8 +2611,19 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        absmode, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int R = 8;
-    hipLaunchKernelGGL((qbuild_quad_kernel<1, R>), dim3(c.P, 128 / (R * 4)), dim3(kQbThreads), 0,
-                       c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    static const int qbt = [] {  // A/B measurements only
+      const char* e = getenv("SVDJ_QBQ_THREADS");
+      return e ? atoi(e) : 256;
+    }();
+    if (qbt == 1024)
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 1024>), dim3(c.P, 128 / (R * 16)), dim3(1024), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    else if (qbt == 512)
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 512>), dim3(c.P, 128 / (R * 8)), dim3(512), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    else
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 256>), dim3(c.P, 128 / (R * 4)), dim3(256), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL(quad_update_kernel, dim3(c.P, 2), dim3(kUpdThreads), 0, c.st,
                        c.qslabs + (size_t)c.P * c.g.qgch * 64 * 64, c.g.qgch, c.T1, c.upd);
@@ -2621,8 +2632,15 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
-    hipLaunchKernelGGL((qbuild_quad_kernel<2, R>), dim3(c.P, 256 / (R * 4)), dim3(kQbThreads), 0,
-                       c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    if (qbt == 1024)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 1024>), dim3(c.P, 256 / (R * 16)), dim3(1024), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    else if (qbt == 512)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 512>), dim3(c.P, 256 / (R * 8)), dim3(512), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    else
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 256>), dim3(c.P, 256 / (R * 4)), dim3(256), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
     SVDJ_LAUNCH_CHECK();
     const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
     if (mma == 2)

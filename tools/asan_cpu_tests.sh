@@ -13,5 +13,8 @@ print(b.build_cpu(asan=True), b.build_dist_asan())") || exit 1
 export SVDJ_CPU_LIB=$CPU SVDJ_DIST_LIB=$DIST
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1
 export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
+# the whole CPU suite unless test paths are given
+WHAT=tests
+for a in "$@"; do case "$a" in tests/*) WHAT= ;; esac; done
 LD_PRELOAD="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libubsan.so)" \
-  python3 -m pytest tests -q -m "not gpu" -p no:cacheprovider "$@"
+  python3 -m pytest $WHAT -q -m "not gpu" -p no:cacheprovider "$@"
