@@ -2426,8 +2426,14 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // the solve is bitwise the two-chain one (same sweeps).  Measured at 128
   // pairs (16384^2 merged, quad off): 4 chunks 4.70 s vs 2 chunks (the
   // target rule) 4.73 s, residual 1.37e-5 vs 1.52e-5 (profiles/r5_gram).
-  const int gram_target = P >= 32 ? 256 : 512;
-  int want = (gram_target + P - 1) / P;
+  // Round 5 (profiles/r5_ab): below 32 pairs, at most ~512 workgroups AND
+  // chunks of at least 512 rows -- rank plans, ms per sweep: 16384^2 P = 8
+  // (8 pairs) 53.5 at 256 rows (512 workgroups, the old rule), 52.9 at 384,
+  // 43.5 at 512, 55.2 at 1024; P = 4 (16 pairs) 100.9 / 82.8 / 83.9 / 86.7 at
+  // 256 / 384 / 512 / 1024 rows; 32768 x 32768 P = 8 (16 pairs) 307 at 1024
+  // rows (512 workgroups) vs 325 at 512 (1024 workgroups).  The EVD sums one
+  // slab per chunk, so short chunks put more slab data on its critical path.
+  int want = P >= 32 ? (256 + P - 1) / P : min((m_pad + 511) / 512, (512 + P - 1) / P);
   if (P >= 64 && want < 4) want = 4;
   static const int forced = [] {  // A/B measurements only
     const char* e = getenv("SVDJ_GRAM_CHUNKS");
@@ -2611,19 +2617,12 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        absmode, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int R = 8;
-    static const int qbt = [] {  // A/B measurements only
-      const char* e = getenv("SVDJ_QBQ_THREADS");
-      return e ? atoi(e) : 256;
-    }();
-    if (qbt == 1024)
-      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 1024>), dim3(c.P, 128 / (R * 16)), dim3(1024), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
-    else if (qbt == 512)
-      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 512>), dim3(c.P, 128 / (R * 8)), dim3(512), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
-    else
-      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 256>), dim3(c.P, 128 / (R * 4)), dim3(256), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    // 1024 threads: one workgroup per pair (phase 1) / two (phase 2), so each
+    // pair's rotation records are staged 1-2 times instead of 4-8 (128-pair
+    // quad step 832 -> 824 us, profiles/r5_ab)
+    constexpr int QBT = 1024, QBW = QBT / SVDJ_WAVE;
+    hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
+                       c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL(quad_update_kernel, dim3(c.P, 2), dim3(kUpdThreads), 0, c.st,
                        c.qslabs + (size_t)c.P * c.g.qgch * 64 * 64, c.g.qgch, c.T1, c.upd);
@@ -2632,15 +2631,8 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
-    if (qbt == 1024)
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 1024>), dim3(c.P, 256 / (R * 16)), dim3(1024), 0,
-                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
-    else if (qbt == 512)
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 512>), dim3(c.P, 256 / (R * 8)), dim3(512), 0,
-                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
-    else
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, 256>), dim3(c.P, 256 / (R * 4)), dim3(256), 0,
-                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT>), dim3(c.P, 256 / (R * QBW)), dim3(QBT), 0,
+                       c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
     SVDJ_LAUNCH_CHECK();
     const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
     if (mma == 2)

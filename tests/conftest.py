@@ -11,6 +11,14 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running test")
+    # pytest-xdist: every worker's torch would otherwise start one thread per
+    # CPU, and N workers oversubscribe the machine N-fold (the CPU emulation
+    # tests then ran 100x slower and hit the 900 s timeout)
+    workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "0") or 0)
+    if workers > 1:
+        import torch
+
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // workers))
 
 
 @pytest.fixture(scope="session")

@@ -103,7 +103,9 @@ def test_quad_step_equals_two_cross_steps(svdj, cuda, nb, m, inner):
     assert r1 == r2 == nb
     assert math.isclose(m1, m2, rel_tol=1e-3)
     if inner == 1:
-        tol = 5e-5
+        # (the cross steps' Gram row chunking sets their rounding: 5e-5 held
+        # with 128-row chunks, 8.3e-5 was seen with 384-row chunks)
+        tol = 2e-4
         torch.testing.assert_close(a1, a2, rtol=tol, atol=tol)
         torch.testing.assert_close(v1, v2, rtol=tol, atol=tol)
         torch.testing.assert_close(d1, d2, rtol=tol, atol=tol)
