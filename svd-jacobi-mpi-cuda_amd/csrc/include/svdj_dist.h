@@ -102,8 +102,8 @@ typedef struct {
                               // (svdj_stop.h; relative mode); 0: only a sweep without
                               // rotations does.  converged (out) = 1 (no rotation) or 2
   int quad;                   // quad steps (two cross steps fused, fp32 W = 64 split-bf16
-                              // apply): 0 auto (one GPU, >= 64 pairs per chain step:
-                              // models/block.py choose_quad), 1 on, 2 off
+                              // apply): 0 auto (>= 32 pairs per chain step, any number of
+                              // GPUs: models/block.py choose_quad), 1 on, 2 off
   int quad_used;              // out
   int merged_used;            // out: 1 = one GPU, the two chains issued as single launches of
                               // twice the pairs (pipeline.run_merged; >= 64 pairs per chain step)

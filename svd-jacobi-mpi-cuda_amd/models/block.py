@@ -85,20 +85,18 @@ def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
 
 
 def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
-    """Quad steps for config quad="auto": on ONE GPU when a chain step holds
-    >= 64 pairs (k // 2 >= 64, 16384^2 and up; the merged one-GPU issue
-    then runs 128-pair quad steps), off otherwise.
+    """Quad steps for config quad="auto": whenever a chain step holds >= 32
+    pairs (k // 2 >= 32), on any number of GPUs; off below.
 
-    Measured on MI355X (profiles/r5_quad), with the round-5 kernels: the six
-    cross Grams read each block once on split-bf16 MFMAs (gram_quad_kernel)
-    and the K = 256 apply keeps T register-resident in a persistent grid
-    (apply_quad_ts_kernel).  16384^2 fp32: 3.69 s vs 4.72 s per solve (18
-    sweeps both; residual 1.07e-5 vs 1.37e-5, orth U/V max 1.53e-5 /
-    7.2e-6 vs 1.53e-5 / 9.3e-6); 128-pair step probe 879 vs 1203 us per
-    step.  With few quads per step the per-workgroup T load and the EVD
-    chain latency dominate: 8192^2 821 vs 678 ms, 4096^2 358 vs 132 ms,
-    16384^2 rank plans P=2/4/8 170/146/192 vs 163/84/53 ms per sweep."""
-    return P == 1 and k // 2 >= 64 and quad_supported(dtype, W, mma, k)
+    Measured on MI355X with the round-5 kernels (one-read split-bf16 quad
+    Gram with a swizzled raw image, T-stationary persistent K = 256 apply,
+    vectorised Gram-space update; profiles/r5_quad2, ms per solve or per
+    full-work sweep, quad on vs off): 1 GPU 16384^2 3.49-3.62 vs 4.70 s,
+    8192^2 637 vs 685 ms; rank plans with 32 pairs per step: 16384^2 P=2
+    144 vs 165, 32768^2 P=4 449 vs 596, 65536^2 P=8 1749 vs 2112.  With 16
+    pairs the EVD chain's latency is exposed and quad steps lose: 16384^2
+    P=4 98.6 vs 84.4 (and P=8, 8 pairs, 192 vs 53 in profiles/r5_quad)."""
+    return k // 2 >= 32 and quad_supported(dtype, W, mma, k)
 
 
 def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:

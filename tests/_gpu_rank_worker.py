@@ -28,7 +28,8 @@ def main():
     timing = os.environ.get("SVDJ_TEST_TIMING", "1") == "1"
     cfg = svdj.SolverConfig(block=W, dtype=torch.float32, chains=chains, comm_timing=timing,
                             precondition="none", progress=True,
-                            exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"))
+                            exchange=os.environ.get("SVDJ_TEST_EXCHANGE", "auto"),
+                            quad=os.environ.get("SVDJ_TEST_QUAD", "auto"))
     solver = DistributedBlockJacobi(cfg, comm)
     g = torch.Generator(device=dev).manual_seed(5)
     m = 4 * n if mode in ("qr", "qrbf16") else n
@@ -49,7 +50,7 @@ def main():
                     "sweeps": res.sweeps, "converged": res.converged, "history": res.history,
                     "backend": comm.backend, "world": comm.world,
                     "exchange": res.info.get("exchange"), "mma": res.info.get("mma"),
-                    "inner_order": res.info.get("inner_order"),
+                    "inner_order": res.info.get("inner_order"), "quad": res.info.get("quad"),
                     "comm": json.dumps(res.info.get("comm"))}, out)
     comm.destroy()
 

@@ -36,9 +36,10 @@ def _port():
 
 
 def _run(P, backend, out, n=1024, W=32, chains=2, mode="otf", timeout=300, exchange="auto",
-         timing=True):
+         timing=True, quad="auto"):
     env = dict(os.environ, SVDJ_SHARED_GPU="1", SVDJ_COMM_BACKEND=backend, OMP_NUM_THREADS="2",
-               SVDJ_TEST_EXCHANGE=exchange, SVDJ_TEST_TIMING="1" if timing else "0")
+               SVDJ_TEST_EXCHANGE=exchange, SVDJ_TEST_TIMING="1" if timing else "0",
+               SVDJ_TEST_QUAD=quad)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={P}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(n), str(W),
            str(chains), mode, str(out)]
@@ -114,6 +115,22 @@ def test_production_default_rccl_matches_gloo(P, tmp_path):
         assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
     _check_accuracy(r)
     assert c["exchanges"] == 2 * (2 * P - 2) * r["sweeps"] and not c["timing"], c
+
+
+def test_quad_steps_rccl_matches_gloo(tmp_path):
+    """Quad steps with exchanges (on by default from 32 pairs per chain step,
+    forced here at test size: n = 4096, 2 ranks, 8 pairs per cross step): the
+    quad pair lists go through the half-buffer remap of every round like the
+    single steps.  RCCL equals the host-synchronised gloo run bitwise and is
+    accurate."""
+    r = _run(2, "nccl", tmp_path / "rccl.pt", n=4096, W=64, timing=False, quad="on")
+    g = _run(2, "gloo", tmp_path / "gloo.pt", n=4096, W=64, timing=False, quad="on",
+             exchange="direct")
+    assert r["quad"] is True and g["quad"] is True, (r["quad"], g["quad"])
+    assert r["sweeps"] == g["sweeps"], (r["history"], g["history"])
+    for k in ("U", "S", "V"):
+        assert torch.equal(r[k], g[k]), (k, float((r[k] - g[k]).abs().max()))
+    _check_accuracy(r)
 
 
 def test_production_config_spread_matches_direct(tmp_path):

@@ -173,3 +173,16 @@ def test_native_engine_production_default_matches_python(tmp_path):
     assert nat["sweeps"] == py["sweeps"], (nat["sweeps"], py["sweeps"])
     assert abs(nat["accuracy"]["residual_rel"] - py["accuracy"]["residual_rel"]) < 1e-8
     assert nat["ms_per_step"] < 1.1 * py["ms_per_step"], (nat["ms_per_step"], py["ms_per_step"])
+
+
+def test_native_quad_steps_two_ranks():
+    """Native engine, 2 RCCL ranks, quad steps forced (--quad on; auto from 32
+    pairs per chain step): converges to fp32 accuracy through the exchanges."""
+    r = subprocess.run([_exe(), "4096", "--np", "2", "--shared-gpu", "--dtype", "f32",
+                        "--input", "dense", "--verify", "--quad", "on", "--timeout", "120"],
+                       capture_output=True, text=True, timeout=240)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and re.search(r"converged: [12]\b", out), out[-4000:]
+    assert "quad steps" in out, out[-3000:]
+    assert _value(out, "||A-USVt||_F/||A||_F:") < 3e-5, out
+    assert _value(out, "||V^TV-I||_F:") < 5e-3, out
