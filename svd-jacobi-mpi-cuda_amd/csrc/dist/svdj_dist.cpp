@@ -841,15 +841,15 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   // 3 = auto: by the pairs of a cross step (half super-blocks)
   const int io = p->inner_order == 3 ? svdj_choose_inner_order(p->dtype, W, h->hk) : p->inner_order;
   h->io = io;
-  // merged issue on one GPU from 64 pairs per chain step, quad steps from 32
-  // pairs on any number of GPUs (the Python engine's rules: distributed.py
-  // merged, models/block.py choose_quad)
-  const char* em = getenv("SVDJ_MERGE_CHAINS");
-  h->merged = p->world == 1 && (em ? atoi(em) == 1 : h->hk >= 64);
+  // quad steps from 32 pairs per chain step on any number of GPUs, merged
+  // issue on one GPU from 64 pairs (32 with quad steps) -- the Python
+  // engine's rules: models/block.py choose_quad, distributed.py merged
   const bool quad_ok = p->dtype == 0 && W == 64 && (p->mma == 1 || p->mma == 2) && h->k % 4 == 0;
   if (p->quad < 0 || p->quad > 2) rc = fail(-2, "quad %d (0 auto, 1 on, 2 off)", p->quad);
   if (p->quad == 1 && !quad_ok) rc = rc ? rc : fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
   h->quad = quad_ok && (p->quad == 1 || (p->quad == 0 && h->hk >= 32));
+  const char* em = getenv("SVDJ_MERGE_CHAINS");
+  h->merged = p->world == 1 && (em ? atoi(em) == 1 : h->hk >= (h->quad ? 32 : 64));
   if (!rc) guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->merged ? h->k : h->k / 2, p->m_pad,
                                       h->quad ? 1 : 0);

@@ -306,17 +306,19 @@ class DistributedBlockJacobi(Solver):
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                               inner_order=inner)
-        # One rank, no exchanges, >= 64 pairs per chain step: the two chains'
-        # parallel tasks merged into single launches of 128+ pairs
-        # (PipelineExecutor.run_merged) -- bitwise the two-chain solve (the
-        # Gram keeps the 64-pair chunking), the EVD latency paid once per step
-        # (profiles/r4_merge).  Smaller steps keep the overlapped chains
-        # (8192^2: 32 pairs per chain, merged +10 %).  SVDJ_MERGE_CHAINS=0/1
+        # One rank, no exchanges, >= 64 pairs per chain step (>= 32 with quad
+        # steps): the two chains' parallel tasks merged into single launches
+        # of twice the pairs (PipelineExecutor.run_merged), the EVD latency
+        # paid once per step (profiles/r4_merge; from 64 pairs bitwise the
+        # two-chain solve, the Gram keeps the chunking).  Single steps of 32
+        # pairs keep the overlapped chains (8192^2 merged +10 %); quad steps
+        # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
+        # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_MERGE_CHAINS=0/1
         # overrides; with exchanges merging was slower at every P.
         env_merge = os.environ.get("SVDJ_MERGE_CHAINS")
         merged = (pipelined and dev.type == "cuda" and
                   (env_merge == "1" if env_merge is not None
-                   else (not comm.distributed and k // 2 >= 64)))
+                   else (not comm.distributed and k // 2 >= (32 if quad else 64))))
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
