@@ -2110,7 +2110,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
@@ -2282,9 +2281,7 @@ constexpr int kGramQThreads = 512;
 struct GramQLds {
   static constexpr int S_BYTES = 2 * 8 * 3 * SVDJ_WAVE * 16;  // 2 k steps x 8 col tiles x 3 parts
   static constexpr int R_BYTES = 8 * 32 * 32 * 4;             // raw 32-row slab, wave w at 4 KB * w
-  // one split image, three raw slabs in flight (the loads, not the MFMAs,
-  // held the double-buffered form: 42 % wait-any)
-  static constexpr int TOTAL = S_BYTES + 3 * R_BYTES;
+  static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
 };
 static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
 __global__ __launch_bounds__(kGramQThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
@@ -2309,9 +2306,9 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   // rows 4 (j ^ (col & 7)) .. + 3: the split's reads (8 rows of one column per
   // lane, lanes at a 128-byte column stride) then spread over all banks
   // instead of piling onto a few (35 % bank-conflict cycles unswizzled)
-  auto dma = [&](int sl) {
+  auto dma = [&](int sl, int buf) {
     const int r0 = r_begin + 32 * sl;
-    char* dst = lds + L::S_BYTES + (sl % 3) * L::R_BYTES + wave * 4096;
+    char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
     const int jr = ((lane & 7) ^ (lane >> 3)) * 4;  // col & 7 == lane >> 3 for every i
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -2321,18 +2318,13 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   f32x16 acc[3], lo[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) acc[j] = lo[j] = Mfma<float>::zero();
-  if (ns > 0) dma(0);
-  if (ns > 1) dma(1);
-  if (ns > 2) dma(2);
-  for (int sl = 0; sl < ns; ++sl) {
-    // own DMA of slab sl landed (younger: the DMAs of sl + 1, sl + 2)
-    const int younger = (sl + 1 < ns ? 4 : 0) + (sl + 2 < ns ? 4 : 0);
-    if (younger == 8) wait_vmcnt<8>();
-    else if (younger == 4) wait_vmcnt<4>();
+  auto slab = [&](int sl, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    if (sl + 1 < ns) wait_vmcnt<4>();
     else wait_vmcnt<0>();
     {  // split column tile `wave` of this slab: rows 16 kk + 8h .. + 7 of column c
-      const float* R = reinterpret_cast<const float*>(lds + L::S_BYTES + (sl % 3) * L::R_BYTES + wave * 4096);
-      bf16x8* Sw = reinterpret_cast<bf16x8*>(lds) + lane;
+      const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
+      bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int rc = 4 * kk + 2 * h;  // row chunks rc, rc + 1 of column c
@@ -2352,9 +2344,7 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // the raw slab is split: refill it three slabs ahead
-    if (sl + 3 < ns) dma(sl + 3);
-    const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds) + lane;
+    const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -2370,9 +2360,13 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
         lo[j] = mfma_split<NP, 1>(xf, yf, lo[j]);
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf[0], yf[0], acc[j], 0, 0, 0);
       }
-    // every wave has read the split image before the next split overwrites it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (sl + 2 < ns) dma(sl + 2, buf);
+  };
+  if (ns > 0) dma(0, 0);
+  if (ns > 1) dma(1, 1);
+  for (int sl = 0; sl < ns; sl += 2) {
+    slab(sl, std::integral_constant<int, 0>{});
+    if (sl + 1 < ns) slab(sl + 1, std::integral_constant<int, 1>{});
   }
   // the wave's three tiles straight to their slabs
 #pragma unroll
