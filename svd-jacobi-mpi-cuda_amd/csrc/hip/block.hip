@@ -2090,8 +2090,8 @@ __global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
 //     flight), splits them into the shared B-fragment image of the tile
 //     (double-buffered, one barrier per tile), runs 16 k blocks x (1 + 5)
 //     MFMAs (leading product and the small ones in two accumulators, as
-//     apply_split_kernel), and rebuilds its own raw values for the delta-form
-//     epilogue Y = X + X (T - I) from that image (the 3-way split is exact).
+//     apply_split_kernel), and reads its own raw values for the delta-form
+//     epilogue Y = X + X (T - I) back from its raw image.
 // Work: the active quads (some step-s or step-(s+1) pair rotated) are listed
 // by every wave with ballots over the skip flags (no extra launch, no host
 // sync); nact active quads x S row slices, S = max(1, grid / nact), are dealt
@@ -2217,29 +2217,20 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
       }
       acc += lo;
-      // 4. own raw values from the image (acc layout: register 4g + i is
-      //    column 8g + 4h + i = k block 2 wave + (g >> 1), lane half g & 1,
-      //    element 4h + i) and the delta-form store, in place
+      // 4. own raw values, still in this wave's raw image R[buf] (its refill,
+      //    tile t + 2, is issued below), and the delta-form store, in place
+      //    (acc layout: register 4g + i is own column 8g + 4h + i, row c)
       {
         const bool isA = t < a_tiles;
         float* const own = isA ? ownA : ownV;
         const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
         const uint32_t st_off = (uint32_t)(4 * h * ld + c) + (uint32_t)r0;
-        const char* Sb = lds + buf * L::S_BYTES;
+        const float* Rr = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int kb = 2 * wave + (g >> 1), ln = c + 32 * (g & 1);
           float v[4];
 #pragma unroll
-          for (int i = 0; i < NP; ++i) {  // x = (x0 + x1) + x2, exact
-            const uint2 u = *reinterpret_cast<const uint2*>(Sb + ((kb * NP + i) * SVDJ_WAVE + ln) * 16 + 8 * h);
-            const float w0 = __uint_as_float(u.x << 16), w1 = __uint_as_float(u.x & 0xffff0000u);
-            const float w2 = __uint_as_float(u.y << 16), w3 = __uint_as_float(u.y & 0xffff0000u);
-            v[0] = i ? v[0] + w0 : w0;
-            v[1] = i ? v[1] + w1 : w1;
-            v[2] = i ? v[2] + w2 : w2;
-            v[3] = i ? v[3] + w3 : w3;
-          }
+          for (int i = 0; i < 4; ++i) v[i] = Rr[(8 * g + 4 * h + i) * 32 + c];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             at_u32(own + (size_t)Mfma<float>::acc_row_uni(4 * g + i) * ld, st_off) = v[i] + acc[4 * g + i];
