@@ -84,6 +84,71 @@ __global__ __launch_bounds__(512) void tiles_k(float* __restrict__ X, int ld, in
   }
 }
 
+// The quad apply's exact load path: each of 8 waves LDS-DMAs its own 32
+// columns of a 32-row tile (global_load_lds_dwordx4, 4 instructions, two
+// tiles ahead), reads them back from LDS and stores the tile in place.
+template <int AHEAD>
+__global__ __launch_bounds__(512) void tiles_dma_k(float* __restrict__ X, int ld, int rows, int SL, float c) {
+  __shared__ __attribute__((aligned(16))) char lds[AHEAD * 8 * 4096];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x / SL, sl = blockIdx.x % SL;
+  const int t0 = sl * (rows / SL) / 32, t1 = t0 + rows / SL / 32;
+  float* own = X + ((size_t)q * 256 + wave * 32) * ld;
+  auto dma = [&](int t) {
+    char* dst = lds + ((t - t0) % AHEAD) * 8 * 4096 + wave * 4096;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(own + (size_t)(8 * i + (lane >> 3)) * ld + t * 32 + (lane & 7) * 4,
+                                       dst + i * 1024, 16, 0, 0);
+  };
+  for (int a = 0; a < AHEAD && t0 + a < t1; ++a) dma(t0 + a);
+  for (int t = t0; t < t1; ++t) {
+    // AHEAD == 2: exactly the apply's wait (younger: DMA of t + 1, stores of
+    // t - 1); otherwise everything (conservative)
+    const int younger = AHEAD == 2 ? (t + 1 < t1 ? 4 : 0) + (t > t0 ? 16 : 0) : 0;
+    if (younger == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (younger == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float* R = reinterpret_cast<const float*>(lds + ((t - t0) % AHEAD) * 8 * 4096 + wave * 4096);
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = R[(2 * j + (lane >> 5)) * 32 + (lane & 31)];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + AHEAD < t1) dma(t + AHEAD);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) own[(size_t)(2 * j + (lane >> 5)) * ld + t * 32 + (lane & 31)] = v[j] * c;
+  }
+}
+
+// Same walk, loads into registers with the DMA's lane map, two tiles in flight
+__global__ __launch_bounds__(512) void tiles_reg_k(float* __restrict__ X, int ld, int rows, int SL, float c) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x / SL, sl = blockIdx.x % SL;
+  const int t0 = sl * (rows / SL) / 32, t1 = t0 + rows / SL / 32;
+  float* own = X + ((size_t)q * 256 + wave * 32) * ld;
+  f32x4 a[4], b[4];
+  auto ld4 = [&](int t, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      v[i] = *reinterpret_cast<const f32x4*>(own + (size_t)(8 * i + (lane >> 3)) * ld + t * 32 + (lane & 7) * 4);
+  };
+  auto st4 = [&](int t, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<f32x4*>(own + (size_t)(8 * i + (lane >> 3)) * ld + t * 32 + (lane & 7) * 4) = v[i] * c;
+  };
+  ld4(t0, a);
+  for (int t = t0; t < t1; t += 2) {
+    if (t + 1 < t1) ld4(t + 1, b);
+    st4(t, a);
+    if (t + 1 < t1) {
+      if (t + 2 < t1) ld4(t + 2, a);
+      st4(t + 1, b);
+    }
+  }
+}
+
 template <typename F>
 static float best_ms(F launch) {
   hipEvent_t e0, e1;
@@ -136,6 +201,22 @@ int main() {
     run_tiles<32>(X, ld, rows, ncol, SL);
     run_tiles<64>(X, ld, rows, ncol, SL);
     run_tiles<128>(X, ld, rows, ncol, SL);
+  }
+  const int nq = ncol / 256;
+  const double bytes = 2.0 * ncol * (double)rows * 4;
+  for (int SL : {4, 8}) {
+    float ms = best_ms([&] {
+      hipLaunchKernelGGL(tiles_reg_k, dim3(nq * SL), dim3(512), 0, 0, X, ld, rows, SL, 1.0f);
+    });
+    printf("{\"case\": \"tiles_reg_applymap\", \"workgroups\": %d, \"ms\": %.3f, \"TB_s\": %.3f}\n", nq * SL, ms, bytes / ms / 1e9);
+    ms = best_ms([&] {
+      hipLaunchKernelGGL((tiles_dma_k<2>), dim3(nq * SL), dim3(512), 0, 0, X, ld, rows, SL, 1.0f);
+    });
+    printf("{\"case\": \"tiles_dma2\", \"workgroups\": %d, \"ms\": %.3f, \"TB_s\": %.3f}\n", nq * SL, ms, bytes / ms / 1e9);
+    ms = best_ms([&] {
+      hipLaunchKernelGGL((tiles_dma_k<1>), dim3(nq * SL), dim3(512), 0, 0, X, ld, rows, SL, 1.0f);
+    });
+    printf("{\"case\": \"tiles_dma1_drain\", \"workgroups\": %d, \"ms\": %.3f, \"TB_s\": %.3f}\n", nq * SL, ms, bytes / ms / 1e9);
   }
   CHECK(hipFree(X));
   CHECK(hipFree(Y));
