@@ -628,6 +628,19 @@ int build_templates(svdj_dist_handle_t* h, int cross_mode) {
 
 }  // namespace
 
+extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int quad_mode,
+                                     int* quad, int* merged) {
+  const bool quad_ok = dtype == 0 && W == 64 && (mma == 1 || mma == 2) && k % 4 == 0;
+  if (quad_mode < 0 || quad_mode > 2) return fail(-2, "quad %d (0 auto, 1 on, 2 off)", quad_mode);
+  if (quad_mode == 1 && !quad_ok)
+    return fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
+  const int hk = k / 2;
+  *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && hk >= 32));
+  const char* em = getenv("SVDJ_MERGE_CHAINS");
+  *merged = world == 1 && (em ? atoi(em) == 1 : hk >= (*quad ? 32 : 64));
+  return 0;
+}
+
 extern "C" int svdj_dist_merged_lists(int k, int quad, int cross_mode, int32_t* pairs, int pcap,
                                       int32_t* modes, int mcap, int32_t* meta) {
   if (k < 4 || k % 2 || (quad && k % 4)) return fail(-2, "bad merged-list args");
@@ -844,12 +857,11 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   // quad steps from 32 pairs per chain step on any number of GPUs, merged
   // issue on one GPU from 64 pairs (32 with quad steps) -- the Python
   // engine's rules: models/block.py choose_quad, distributed.py merged
-  const bool quad_ok = p->dtype == 0 && W == 64 && (p->mma == 1 || p->mma == 2) && h->k % 4 == 0;
-  if (p->quad < 0 || p->quad > 2) rc = fail(-2, "quad %d (0 auto, 1 on, 2 off)", p->quad);
-  if (p->quad == 1 && !quad_ok) rc = rc ? rc : fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
-  h->quad = quad_ok && (p->quad == 1 || (p->quad == 0 && h->hk >= 32));
-  const char* em = getenv("SVDJ_MERGE_CHAINS");
-  h->merged = p->world == 1 && (em ? atoi(em) == 1 : h->hk >= (h->quad ? 32 : 64));
+  int quad = 0, merged = 0;
+  const int dr = svdj_dist_issue_rules(p->world, p->dtype, W, p->mma, h->k, p->quad, &quad, &merged);
+  if (dr < 0) rc = dr;
+  h->quad = quad != 0;
+  h->merged = merged != 0;
   if (!rc) guard(build_templates(h, io == 2 ? 3 : (io ? 2 : 0)));
   h->wsb = svdj_block_workspace_bytes(p->dtype, W, h->merged ? h->k : h->k / 2, p->m_pad,
                                       h->quad ? 1 : 0);

@@ -132,6 +132,15 @@ int svdj_dist_solve(svdj_dist_problem* p, void* sigma);
 // half}; halves are slot*2 + half.  Returns the group count (<= cap) or <0.
 int svdj_dist_plan(int world, int rank, int32_t* out, int cap);
 
+// Issue rules of a rank with k W-blocks per super-block (host only): quad
+// steps (quad_mode 0 auto / 1 on / 2 off; auto = from 32 pairs per chain
+// step, fp32 W = 64 split-bf16 apply, k % 4 == 0) and, on one GPU, the
+// merged issue (from 64 pairs per chain step, 32 with quad steps;
+// SVDJ_MERGE_CHAINS=0/1 overrides) -- models/block.py choose_quad and
+// parallel/distributed.py choose_merged.  Returns 0 or <0.
+int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int quad_mode, int* quad,
+                          int* merged);
+
 // One-GPU merged issue (host only, for tests): the pair lists of the three
 // merged task groups of a sweep with k blocks per super-block (rr0+rr1,
 // T00+T11, T01+T10; local block ids), concatenated step by step; modes[] the

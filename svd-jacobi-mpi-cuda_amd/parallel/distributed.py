@@ -46,6 +46,17 @@ from .pipeline import PipelineExecutor, sweep_plan
 from .schedule import distributed_sweep_plan, tournament
 
 
+def choose_merged(P: int, k: int, quad: bool) -> bool:
+    """One-GPU merged issue (PipelineExecutor.run_merged) for k W-blocks per
+    super-block: from 64 pairs per chain step, 32 with quad steps (measured:
+    see the comment at its use in DistributedBlockJacobi._solve).
+    SVDJ_MERGE_CHAINS=0/1 overrides.  libsvdj_dist: svdj_dist_issue_rules."""
+    env = os.environ.get("SVDJ_MERGE_CHAINS")
+    if env is not None:
+        return env == "1"
+    return P == 1 and k // 2 >= (32 if quad else 64)
+
+
 class DistributedBlockJacobi(Solver):
     name = "distributed-block"
 
@@ -315,10 +326,8 @@ class DistributedBlockJacobi(Solver):
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
         # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_MERGE_CHAINS=0/1
         # overrides; with exchanges merging was slower at every P.
-        env_merge = os.environ.get("SVDJ_MERGE_CHAINS")
-        merged = (pipelined and dev.type == "cuda" and
-                  (env_merge == "1" if env_merge is not None
-                   else (not comm.distributed and k // 2 >= (32 if quad else 64))))
+        merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
+                                                                    k, quad)
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)

@@ -342,3 +342,37 @@ def test_native_merged_lists_match_python(k, quad):
     assert np.array_equal(pairs[:n], want)
     assert modes[:len(want_modes)].tolist() == want_modes
     assert meta.tolist() == want_meta
+
+
+def test_native_issue_rules_match_python(monkeypatch):
+    """Quad steps and the merged one-GPU issue are decided by the same rules in
+    libsvdj_dist (svdj_dist_issue_rules) and the Python engine
+    (models.block.resolve_quad, parallel.distributed.choose_merged)."""
+    import ctypes
+
+    import torch
+
+    from svdj.models.block import resolve_quad
+    from svdj.ops import _native as nat
+    from svdj.parallel.distributed import choose_merged
+
+    monkeypatch.delenv("SVDJ_MERGE_CHAINS", raising=False)
+    lib = nat.dist_lib()
+    q, mg = ctypes.c_int32(), ctypes.c_int32()
+    for world in (1, 2, 8):
+        for dt, code in ((torch.float32, 0), (torch.float64, 1)):
+            for W in (32, 64):
+                for mma, mcode in (("native", 0), ("bf16x6", 1), ("bf16x3", 2)):
+                    for k in (8, 16, 30, 32, 62, 64, 128, 256):
+                        for mode, mc in (("auto", 0), ("on", 1), ("off", 2)):
+                            rc = lib.svdj_dist_issue_rules(world, code, W, mcode, k, mc,
+                                                           ctypes.byref(q), ctypes.byref(mg))
+                            try:
+                                want_q = resolve_quad(mode, dt, W, mma, k, world)
+                            except ValueError:
+                                assert rc < 0, (world, dt, W, mma, k, mode)
+                                continue
+                            assert rc == 0, (world, dt, W, mma, k, mode)
+                            want_m = choose_merged(world, k, want_q)
+                            assert (bool(q.value), bool(mg.value)) == (want_q, want_m), \
+                                (world, dt, W, mma, k, mode)
