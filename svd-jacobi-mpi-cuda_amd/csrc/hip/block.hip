@@ -2251,159 +2251,6 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
   }
 }
 
-// One wave per SIMD form of the T-stationary apply (A/B, SVDJ_QUAD_APPLY=w4).
-// 4 waves with 512 registers each: wave w owns W-block w of [a b c d] (64
-// output columns, two column tiles) and its split T - I slice (384 VGPRs);
-// one B-fragment read of a k block feeds both tiles (half the LDS reads of
-// the 8-wave form) and the next k block's fragments are read while the 12
-// MFMAs of this one run.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_w4() {
-  if constexpr (N == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-  else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-constexpr int kQuadW4Threads = 256;
-__global__ __launch_bounds__(kQuadW4Threads) __attribute__((amdgpu_waves_per_eu(1, 1))) void
-apply_quad_w4_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
-                     int v_tiles, const int32_t* __restrict__ pairs, int nq,
-                     const bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
-                     const int32_t* __restrict__ skip2) {
-  constexpr int NP = 3;
-  constexpr int S_BYTES = 16 * NP * SVDJ_WAVE * 16;  // split image of a 32-row tile (48 KB)
-  constexpr int R_WAVE = 64 * 32 * 4;                // raw 64 columns x 32 rows of a wave (8 KB)
-  constexpr int R_BYTES = 4 * R_WAVE;
-  __shared__ __attribute__((aligned(16))) char lds[2 * S_BYTES + 2 * R_BYTES];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = lane & 31, h = lane >> 5;
-  auto active = [&](int q) -> bool {
-    if (q >= nq) return false;
-    return (skip1[2 * q] & skip1[2 * q + 1] & skip2[2 * q] & skip2[2 * q + 1]) == 0;
-  };
-  int nact = 0;
-  for (int b0 = 0; b0 < nq; b0 += SVDJ_WAVE) nact += __popcll(__ballot(active(b0 + lane)));
-  if (nact == 0) return;
-  const int G = (int)gridDim.x;
-  const int S = G / nact > 1 ? G / nact : 1;
-  const int nitems = nact * S, nt = a_tiles + v_tiles;
-  for (int item = blockIdx.x; item < nitems; item += G) {
-    const int qi = item / S, sl = item % S;
-    int q = 0;
-    for (int b0 = 0, seen = 0; b0 < nq; b0 += SVDJ_WAVE) {
-      const bool a = active(b0 + lane);
-      const unsigned long long m = __ballot(a);
-      const int cnt = __popcll(m);
-      if (seen <= qi && qi < seen + cnt) {
-        const int pre = __popcll(m & ((1ull << lane) - 1ull));
-        q = b0 + __ffsll((long long)__ballot(a && pre == qi - seen)) - 1;
-      }
-      seen += cnt;
-    }
-    q = __builtin_amdgcn_readfirstlane(q);
-    const int t0 = (int)((long long)sl * nt / S), t1 = (int)((long long)(sl + 1) * nt / S);
-    bf16x8 qf[2][16][NP];  // column tiles 2 wave, 2 wave + 1
-    {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bf16x8* tp = Ts + ((size_t)q * 16 * 8 + 2 * wave + j) * NP * SVDJ_WAVE + lane;
-#pragma unroll
-        for (int kb = 0; kb < 16; ++kb)
-#pragma unroll
-          for (int p = 0; p < NP; ++p) qf[j][kb][p] = tp[(kb * 8 * NP + p) * SVDJ_WAVE];
-      }
-    }
-    const int32_t* qp = pairs + 4 * q;
-    const int col0 = __builtin_amdgcn_readfirstlane(qp[(wave & 1) * 2 + (wave >> 1)] * 64);
-    float* const ownA = A + (size_t)col0 * lda;
-    float* const ownV = V ? V + (size_t)col0 * ldv : nullptr;
-    auto dma = [&](int t, int buf) {  // raw tile t, own 64 columns -> R[buf] (8 x 1 KB)
-      const bool isA = t < a_tiles;
-      const float* base = isA ? ownA : ownV;
-      const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
-      char* dst = lds + 2 * S_BYTES + buf * R_BYTES + wave * R_WAVE;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_global_load_lds(base + (size_t)(8 * i + (lane >> 3)) * ld + r0 + (lane & 7) * 4,
-                                         dst + i * 1024, 16, 0, 0);
-    };
-    auto tile = [&](int t, auto bufc) {
-      constexpr int buf = decltype(bufc)::value;
-      const int younger = (t > t0 ? 32 : 0) + (t + 1 < t1 ? 8 : 0);
-      if (younger == 40) wait_vmcnt_w4<40>();
-      else if (younger == 32) wait_vmcnt_w4<32>();
-      else if (younger == 8) wait_vmcnt_w4<8>();
-      else wait_vmcnt_w4<0>();
-      const float* R = reinterpret_cast<const float*>(lds + 2 * S_BYTES + buf * R_BYTES + wave * R_WAVE);
-      {  // split own 64 columns (k blocks 4 wave .. 4 wave + 3)
-        bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * S_BYTES) + lane;
-#pragma unroll
-        for (int kbl = 0; kbl < 4; ++kbl) {
-          bf16x8 parts[NP];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            __bf16 pp[NP];
-            split_bf16<NP>(R[(16 * kbl + 8 * h + e) * 32 + c], pp);
-#pragma unroll
-            for (int i = 0; i < NP; ++i) parts[i][e] = pp[i];
-          }
-#pragma unroll
-          for (int i = 0; i < NP; ++i) Sw[((4 * wave + kbl) * NP + i) * SVDJ_WAVE] = parts[i];
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * S_BYTES) + lane;
-      f32x16 acc[2], lo[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = lo[j] = Mfma<float>::zero();
-      bf16x8 xs[NP], xn[NP];
-#pragma unroll
-      for (int i = 0; i < NP; ++i) xs[i] = Sr[i * SVDJ_WAVE];
-#pragma unroll
-      for (int kb = 0; kb < 16; ++kb) {
-        if (kb + 1 < 16) {
-#pragma unroll
-          for (int i = 0; i < NP; ++i) xn[i] = Sr[((kb + 1) * NP + i) * SVDJ_WAVE];
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          lo[j] = mfma_split<NP, 1>(qf[j][kb], xs, lo[j]);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[j][kb][0], xs[0], acc[j], 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < NP; ++i) xs[i] = xn[i];
-      }
-      {  // delta-form epilogue from the raw image, in place
-        const bool isA = t < a_tiles;
-        float* const own = isA ? ownA : ownV;
-        const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
-        const uint32_t st_off = (uint32_t)(4 * h * ld + c) + (uint32_t)r0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const f32x16 v = acc[j] + lo[j];
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              at_u32(own + (size_t)(32 * j + Mfma<float>::acc_row_uni(4 * g + i)) * ld, st_off) =
-                  R[(32 * j + 8 * g + 4 * h + i) * 32 + c] + v[4 * g + i];
-        }
-      }
-      if (t + 2 < t1) dma(t + 2, buf);
-    };
-    if (t0 < t1) dma(t0, 0);
-    if (t0 + 1 < t1) dma(t0 + 1, 1);
-    for (int t = t0; t < t1; t += 2) {
-      tile(t, std::integral_constant<int, 0>{});
-      if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
-
 // The six cross Grams of a quad step, every block read ONCE (round 5).  The
 // round-4 form computed them as 3P independent f32-MFMA slabs, each reading
 // its two blocks: every block of a quad was read three times and the f32
@@ -2880,15 +2727,7 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
       }
       // T-stationary persistent apply (apply_quad_ts_kernel)
       const int nq = c.P / 2, at = c.m_pad / 32, vt = c.V ? c.n_v / 32 : 0;
-      static const bool w4 = [] {  // A/B measurements only
-        const char* e = getenv("SVDJ_QUAD_APPLY");
-        return e && e[0] == 'w';
-      }();
-      if (mma == 1 && w4)
-        hipLaunchKernelGGL(apply_quad_w4_kernel, dim3(kQuadTsGrid), dim3(kQuadW4Threads), 0,
-                           c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b]);
-      else if (mma == 1)
+      if (mma == 1)
         hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
                            c.skip2[b]);
