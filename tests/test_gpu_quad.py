@@ -179,6 +179,27 @@ def test_svd_quad_end_to_end(svdj, cuda, quad):
     assert rep["orth_u_fro"] < 1.5e-3 and rep["orth_v_fro"] < 2e-4, rep
 
 
+def test_svd_quad_without_v_and_bf16(svdj, cuda):
+    """Quad steps without V (jobv = NoVec: the apply's V tiles are skipped)
+    give bitwise the singular values of the AllVec solve (V never feeds back
+    into A); and the bf16 problem mode's 2-way split runs quad steps
+    (apply_quad_ts_kernel<2>) to bf16-level accuracy."""
+    from svdj.config import SVDOptions
+    from svdj.parallel import DistributedBlockJacobi
+    A = svdj.utils.inputs.random_dense(1100, 1024, dtype=torch.float64, seed=8).to(cuda)
+    cfg = svdj.SolverConfig(dtype=torch.float32, block=64, mma="bf16x6", quad="on")
+    full = DistributedBlockJacobi(cfg).solve(A)
+    nov = DistributedBlockJacobi(cfg).solve(A, jobv=SVDOptions.NoVec)
+    assert nov.info["quad"] and nov.V is None
+    assert full.sweeps == nov.sweeps and torch.equal(full.S, nov.S)
+    cfg16 = svdj.SolverConfig(dtype=torch.bfloat16, block=64, quad="on")
+    r16 = DistributedBlockJacobi(cfg16).solve(A.to(torch.bfloat16))
+    assert r16.converged and r16.info["quad"] and r16.info["mma"] == "bf16x3", r16.info
+    ref = torch.linalg.svdvals(A.to(torch.bfloat16).double().cpu())
+    got = torch.sort(r16.S.double().cpu(), descending=True).values
+    assert float((got - ref).abs().max() / ref[0]) < 1e-4
+
+
 # ---- pair-count-selected variants of the per-step kernels (VERDICT r3 #5):
 # qbuild_kernel<T, W, 16> from 64 pairs per step, the Gram geometry from 32
 # pairs; the other kernel tests use 2 pairs.
