@@ -628,14 +628,14 @@ int build_templates(svdj_dist_handle_t* h, int cross_mode) {
 
 }  // namespace
 
-extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int quad_mode,
-                                     int* quad, int* merged) {
+extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int m_pad,
+                                     int quad_mode, int* quad, int* merged) {
   const bool quad_ok = dtype == 0 && W == 64 && (mma == 1 || mma == 2) && k % 4 == 0;
   if (quad_mode < 0 || quad_mode > 2) return fail(-2, "quad %d (0 auto, 1 on, 2 off)", quad_mode);
   if (quad_mode == 1 && !quad_ok)
     return fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
   const int hk = k / 2;
-  *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && hk >= 32));
+  *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && (hk >= 32 || (hk >= 16 && m_pad >= 16384))));
   const char* em = getenv("SVDJ_MERGE_CHAINS");
   *merged = world == 1 && (em ? atoi(em) == 1 : hk >= (*quad ? 32 : 64));
   return 0;
@@ -858,7 +858,8 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
   // issue on one GPU from 64 pairs (32 with quad steps) -- the Python
   // engine's rules: models/block.py choose_quad, distributed.py merged
   int quad = 0, merged = 0;
-  const int dr = svdj_dist_issue_rules(p->world, p->dtype, W, p->mma, h->k, p->quad, &quad, &merged);
+  const int dr = svdj_dist_issue_rules(p->world, p->dtype, W, p->mma, h->k, p->m_pad, p->quad,
+                                       &quad, &merged);
   if (dr < 0) rc = dr;
   h->quad = quad != 0;
   h->merged = merged != 0;

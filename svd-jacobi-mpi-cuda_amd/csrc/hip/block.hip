@@ -2251,6 +2251,31 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
   }
 }
 
+// The quad step's Grams summed over their row chunks, spread over 4 x 3P
+// workgroups: fp64 sums in chunk order rounded once -- bitwise what
+// evd_cross_kernel and quad_update_kernel compute from the chunks -- so that
+// with many chunks (few quads: 64 at 4 quads) the latency-bound consumers,
+// one workgroup per pair, read one slab instead of all chunks (8-GPU plan:
+// quad_update 334 us per launch reading 64 chunks, profiles/r5_quad2).
+constexpr int kRedThreads = 256;
+__global__ __launch_bounds__(kRedThreads) void slab_reduce_kernel(const float* __restrict__ in,
+                                                                  int gch, float* __restrict__ out) {
+  constexpr int W = 64, E4 = W * W / 4;
+  const int slab = blockIdx.x, e4 = blockIdx.y * kRedThreads + threadIdx.x;
+  const float4* p = reinterpret_cast<const float4*>(in) + (size_t)slab * gch * E4 + e4;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < gch; ++k) {
+    const float4 v = p[(size_t)k * E4];
+    s0 += (double)v.x;
+    s1 += (double)v.y;
+    s2 += (double)v.z;
+    s3 += (double)v.w;
+  }
+  reinterpret_cast<float4*>(out)[(size_t)slab * E4 + e4] =
+      make_float4((float)s0, (float)s1, (float)s2, (float)s3);
+}
+
 // The six cross Grams of a quad step, every block read ONCE (round 5).  The
 // round-4 form computed them as 3P independent f32-MFMA slabs, each reading
 // its two blocks: every block of a quad was read three times and the f32
@@ -2475,6 +2500,7 @@ static size_t quad_bytes(int P, int m_pad) {
   const size_t kstride = rup256((size_t)P * sizeof(int32_t));
   const size_t tstride = rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float));
   return rup256((size_t)3 * P * g.qgch * W * W * sizeof(float)) +
+         rup256((size_t)3 * P * W * W * sizeof(float)) +
          rup256((size_t)P * 4 * W * W * sizeof(double)) + rup256((size_t)P * W * W * sizeof(float)) +
          4 * tstride + 4 * kstride;
 }
@@ -2511,6 +2537,7 @@ struct Chain {
   int32_t* nsteps;
   // quad steps (has_quad)
   float* qslabs;
+  float* qred;  // the 3P Grams summed over their row chunks (when qgch > 4)
   double* T1;
   float* upd;
   float* Tq;
@@ -2561,6 +2588,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   c.nsteps = (int32_t*)w;
   w += kstride;
   c.qslabs = nullptr;
+  c.qred = nullptr;
   c.T1 = nullptr;
   c.upd = nullptr;
   c.Tq = nullptr;
@@ -2569,6 +2597,8 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   if (quad) {
     c.qslabs = (float*)w;
     w += rup256((size_t)3 * P * c.g.qgch * W * W * sizeof(float));
+    c.qred = (float*)w;
+    w += rup256((size_t)3 * P * W * W * sizeof(float));
     c.T1 = (double*)w;
     w += rup256((size_t)P * 4 * W * W * sizeof(double));
     c.upd = (float*)w;
@@ -2603,8 +2633,17 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     hipLaunchKernelGGL(gram_quad_kernel, dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0, c.st,
                        c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
     SVDJ_LAUNCH_CHECK();
+    // many row chunks (few quads): sum them once, wide, for both consumers
+    const bool red = c.g.qgch > 4;
+    const float* gs = red ? c.qred : c.qslabs;
+    const int gn = red ? 1 : c.g.qgch;
+    if (red) {
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(3 * c.P, 64 * 64 / 4 / kRedThreads),
+                         dim3(kRedThreads), 0, c.st, c.qslabs, c.g.qgch, c.qred);
+      SVDJ_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
-                       pr, c.qslabs, c.g.qgch, c.D, c.rec, c.nsteps, c.skip1[b], (float)tol,
+                       pr, gs, gn, c.D, c.rec, c.nsteps, c.skip1[b], (float)tol,
                        absmode, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int R = 8;
@@ -2616,7 +2655,7 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL(quad_update_kernel, dim3(c.P, 2), dim3(kUpdThreads), 0, c.st,
-                       c.qslabs + (size_t)c.P * c.g.qgch * 64 * 64, c.g.qgch, c.T1, c.upd);
+                       gs + (size_t)c.P * gn * 64 * 64, gn, c.T1, c.upd);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL((evd_cross_kernel<float, 64>), dim3(c.P), dim3(cross_threads<64>()), 0, c.st,
                        pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,

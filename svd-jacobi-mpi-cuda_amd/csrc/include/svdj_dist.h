@@ -102,8 +102,9 @@ typedef struct {
                               // (svdj_stop.h; relative mode); 0: only a sweep without
                               // rotations does.  converged (out) = 1 (no rotation) or 2
   int quad;                   // quad steps (two cross steps fused, fp32 W = 64 split-bf16
-                              // apply): 0 auto (>= 32 pairs per chain step, any number of
-                              // GPUs: models/block.py choose_quad), 1 on, 2 off
+                              // apply): 0 auto (>= 32 pairs per chain step, 16 on columns of
+                              // >= 16384 rows, any number of GPUs: models/block.py
+                              // choose_quad), 1 on, 2 off
   int quad_used;              // out
   int merged_used;            // out: 1 = one GPU, the two chains issued as single launches of
                               // twice the pairs (pipeline.run_merged; >= 64 pairs per chain step)
@@ -134,12 +135,13 @@ int svdj_dist_plan(int world, int rank, int32_t* out, int cap);
 
 // Issue rules of a rank with k W-blocks per super-block (host only): quad
 // steps (quad_mode 0 auto / 1 on / 2 off; auto = from 32 pairs per chain
-// step, fp32 W = 64 split-bf16 apply, k % 4 == 0) and, on one GPU, the
+// step, or 16 on columns of >= 16384 rows; fp32 W = 64 split-bf16 apply,
+// k % 4 == 0) and, on one GPU, the
 // merged issue (from 64 pairs per chain step, 32 with quad steps;
 // SVDJ_MERGE_CHAINS=0/1 overrides) -- models/block.py choose_quad and
 // parallel/distributed.py choose_merged.  Returns 0 or <0.
-int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int quad_mode, int* quad,
-                          int* merged);
+int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int m_pad, int quad_mode,
+                          int* quad, int* merged);
 
 // One-GPU merged issue (host only, for tests): the pair lists of the three
 // merged task groups of a sweep with k blocks per super-block (rr0+rr1,

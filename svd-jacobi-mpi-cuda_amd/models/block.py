@@ -84,22 +84,28 @@ def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
     return dtype == torch.float32 and W == 64 and mma in ("bf16x6", "bf16x3") and k % 4 == 0
 
 
-def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
-    """Quad steps for config quad="auto": whenever a chain step holds >= 32
-    pairs (k // 2 >= 32), on any number of GPUs; off below.
+def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int = 0) -> bool:
+    """Quad steps for config quad="auto", on any number of GPUs: when a chain
+    step holds >= 32 pairs (k // 2 >= 32), or >= 16 pairs on columns of at
+    least 16384 rows; off below.
 
     Measured on MI355X with the round-5 kernels (one-read split-bf16 quad
-    Gram with a swizzled raw image, T-stationary persistent K = 256 apply,
-    vectorised Gram-space update; profiles/r5_quad2, ms per solve or per
-    full-work sweep, quad on vs off): 1 GPU 16384^2 3.49-3.62 vs 4.70 s,
-    8192^2 637 vs 685 ms; rank plans with 32 pairs per step: 16384^2 P=2
-    144 vs 165, 32768^2 P=4 449 vs 596, 65536^2 P=8 1749 vs 2112.  With 16
-    pairs the EVD chain's latency is exposed and quad steps lose: 16384^2
-    P=4 98.6 vs 84.4 (and P=8, 8 pairs, 192 vs 53 in profiles/r5_quad)."""
-    return k // 2 >= 32 and quad_supported(dtype, W, mma, k)
+    Gram with a swizzled raw image, a wide chunk reduction when it has many
+    row chunks, T-stationary persistent K = 256 apply, vectorised Gram-space
+    update; profiles/r5_quad2, ms per solve or per full-work sweep, quad on
+    vs off): 1 GPU 16384^2 3.44-3.62 vs 4.70 s, 8192^2 637 vs 685 ms; rank
+    plans with 32 pairs per step: 16384^2 P=2 137 vs 165, 32768^2 P=4 449 vs
+    596, 65536^2 P=8 1749 vs 2112; with 16 pairs: 16384^2 P=4 78.3 vs 85.0,
+    32768^2 P=8 223 vs 324, but 8192^2 P=2 28.5 vs 27.7 and 4096^2 on one GPU
+    158 vs 136 ms (short columns: the longer EVD chain is exposed); with 8
+    pairs quad steps lose (16384^2 P=8 57 vs 43)."""
+    if not quad_supported(dtype, W, mma, k):
+        return False
+    return k // 2 >= 32 or (k // 2 >= 16 and m_pad >= 16384)
 
 
-def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int) -> bool:
+def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int,
+                 m_pad: int = 0) -> bool:
     if mode == "off":
         return False
     if mode == "on":
@@ -107,7 +113,7 @@ def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int
             raise ValueError(f"quad steps need fp32, W=64, a split-bf16 apply and k % 4 == 0 "
                              f"(dtype={dtype}, W={W}, mma={mma}, k={k})")
         return True
-    return choose_quad(dtype, W, mma, k, P)
+    return choose_quad(dtype, W, mma, k, P, m_pad)
 
 
 def resolve_inner_order(order: str, W: int, pairs_per_step: int,

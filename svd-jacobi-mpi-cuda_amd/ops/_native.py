@@ -196,7 +196,7 @@ def dist_lib():
         _sig(lib, "svdj_dist_solve", c_int, [C.POINTER(DistProblem), c_void_p])
         _sig(lib, "svdj_dist_storage_cols", c_int, [c_int, c_int])
         _sig(lib, "svdj_dist_issue_rules", c_int,
-             [c_int, c_int, c_int, c_int, c_int, c_int, c_i32_p, c_i32_p])
+             [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_i32_p, c_i32_p])
         _sig(lib, "svdj_dist_merged_lists", c_int,
              [c_int, c_int, c_int, c_i32_p, c_int, c_i32_p, c_int, c_i32_p])
         _sig(lib, "svdj_dist_handle_create", c_int, [C.POINTER(DistProblem), C.POINTER(c_void_p)])

@@ -244,7 +244,7 @@ class DistributedBlockJacobi(Solver):
         g = comm.rank
         tour = tournament(P)
         pipelined = cfg.chains == 2
-        quad = pipelined and resolve_quad(cfg.quad, dtype, W, mma, k, P)
+        quad = pipelined and resolve_quad(cfg.quad, dtype, W, mma, k, P, m_pad)
         if pipelined:
             splan = sweep_plan(P, k, tour.xslot[:, g], quad=quad)
         else:

@@ -363,12 +363,14 @@ def test_native_issue_rules_match_python(monkeypatch):
         for dt, code in ((torch.float32, 0), (torch.float64, 1)):
             for W in (32, 64):
                 for mma, mcode in (("native", 0), ("bf16x6", 1), ("bf16x3", 2)):
-                    for k in (8, 16, 30, 32, 62, 64, 128, 256):
+                    for k, m_pad in ((8, 16384), (16, 8192), (16, 16384), (30, 32768),
+                                     (32, 4096), (32, 16384), (62, 8192), (64, 8192),
+                                     (128, 16384), (256, 65536)):
                         for mode, mc in (("auto", 0), ("on", 1), ("off", 2)):
-                            rc = lib.svdj_dist_issue_rules(world, code, W, mcode, k, mc,
+                            rc = lib.svdj_dist_issue_rules(world, code, W, mcode, k, m_pad, mc,
                                                            ctypes.byref(q), ctypes.byref(mg))
                             try:
-                                want_q = resolve_quad(mode, dt, W, mma, k, world)
+                                want_q = resolve_quad(mode, dt, W, mma, k, world, m_pad)
                             except ValueError:
                                 assert rc < 0, (world, dt, W, mma, k, mode)
                                 continue
