@@ -2725,24 +2725,8 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
   }
   SVDJ_LAUNCH_CHECK();
   if (mode == 3) {
-    const T* es = c.slabs;
-    int en = c.g.gchunks;
-    if constexpr (sizeof(T) == 4 && W == 64) {
-      static const int red_min = [] {  // A/B measurements only
-        const char* e = getenv("SVDJ_EVD_RED");
-        return e ? atoi(e) : 0;
-      }();
-      if (red_min > 0 && en >= red_min) {  // the slab area has room for P reduced slabs
-        float* out = (float*)c.slabs + (size_t)c.P * en * W * W;
-        hipLaunchKernelGGL(slab_reduce_kernel, dim3(c.P, W * W / 4 / kRedThreads),
-                           dim3(kRedThreads), 0, c.st, (const float*)c.slabs, en, out);
-        SVDJ_LAUNCH_CHECK();
-        es = (const T*)out;
-        en = 1;
-      }
-    }
     hipLaunchKernelGGL((evd_cross_kernel<T, W>), dim3(c.P), dim3(cross_threads<W>()), 0, c.st, pr,
-                       es, en, c.D, c.rec, c.nsteps, c.skipb[b], (T)tol, absmode,
+                       c.slabs, c.g.gchunks, c.D, c.rec, c.nsteps, c.skipb[b], (T)tol, absmode,
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int RL = W == 64 ? 16 : 8;  // one workgroup per pair
