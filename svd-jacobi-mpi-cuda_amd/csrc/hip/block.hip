@@ -2651,6 +2651,15 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     // pair's rotation records are staged 1-2 times instead of 4-8 (128-pair
     // quad step 832 -> 824 us, profiles/r5_ab)
     constexpr int QBT = 1024, QBW = QBT / SVDJ_WAVE;
+    static const int qb_small = [] {  // A/B measurements only
+      const char* e = getenv("SVDJ_QBQ_SMALL");
+      return e ? atoi(e) : 0;
+    }();
+    const bool lat = qb_small > 0 && c.P < qb_small;  // few pairs: latency, 2 rows per lane
+    if (lat)
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, 2, 1024>), dim3(c.P, 128 / (2 * 16)), dim3(1024), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    else
     hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
                        c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     SVDJ_LAUNCH_CHECK();
@@ -2661,6 +2670,10 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
+    if (lat)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, 1024>), dim3(c.P, 256 / (2 * 16)), dim3(1024), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    else
     hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT>), dim3(c.P, 256 / (R * QBW)), dim3(QBT), 0,
                        c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
     SVDJ_LAUNCH_CHECK();
