@@ -2651,17 +2651,16 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     // pair's rotation records are staged 1-2 times instead of 4-8 (128-pair
     // quad step 832 -> 824 us, profiles/r5_ab)
     constexpr int QBT = 1024, QBW = QBT / SVDJ_WAVE;
-    static const int qb_small = [] {  // A/B measurements only
-      const char* e = getenv("SVDJ_QBQ_SMALL");
-      return e ? atoi(e) : 0;
-    }();
-    const bool lat = qb_small > 0 && c.P < qb_small;  // few pairs: latency, 2 rows per lane
+    // below 64 pairs the Q builds are on the latency path: 2 rows per lane
+    // (16384^2 rank plans, ms per sweep: P = 4 76.9 -> 72.5, P = 2 131.9 ->
+    // 130.0, profiles/r5_quad2/reduce)
+    const bool lat = c.P < 64;
     if (lat)
-      hipLaunchKernelGGL((qbuild_quad_kernel<1, 2, 1024>), dim3(c.P, 128 / (2 * 16)), dim3(1024), 0,
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, 2, QBT>), dim3(c.P, 128 / (2 * QBW)), dim3(QBT), 0,
                          c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     else
-    hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
-                       c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     SVDJ_LAUNCH_CHECK();
     hipLaunchKernelGGL(quad_update_kernel, dim3(c.P, 2), dim3(kUpdThreads), 0, c.st,
                        gs + (size_t)c.P * gn * 64 * 64, gn, c.T1, c.upd);
@@ -2671,11 +2670,11 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     if (lat)
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, 1024>), dim3(c.P, 256 / (2 * 16)), dim3(1024), 0,
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, QBT>), dim3(c.P, 256 / (2 * QBW)), dim3(QBT), 0,
                          c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
     else
-    hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT>), dim3(c.P, 256 / (R * QBW)), dim3(QBT), 0,
-                       c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT>), dim3(c.P, 256 / (R * QBW)), dim3(QBT), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
     SVDJ_LAUNCH_CHECK();
     const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
     if (mma == 2)
