@@ -2745,14 +2745,13 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
     // 16 rows per lane from 64 pairs per step; at 32 pairs 4 rows per lane is
     // faster (1 GPU 8192^2 709 -> 672 ms, 16384^2 P=2 plan 171.4 -> 169.1 ms per
     // sweep; 1 GPU 16384^2 (64 pairs) equal at 4/8/16, profiles/r3_s3/qbuild)
-    static const int qb2 = [] {  // A/B measurements only
-      const char* e = getenv("SVDJ_QB2");
-      return e ? atoi(e) : 0;
-    }();
+    // below 16 pairs (8-GPU plans) 2 rows per lane: a shorter rotation chain
+    // per lane on the latency path (16384^2 P = 8: 44.1-44.5 -> 43.6-43.7 ms
+    // per sweep, profiles/r5_ab/qb2)
     if (c.P >= 64)
       hipLaunchKernelGGL((qbuild_kernel<T, W, RL>), dim3(c.P, qbuild_blocks<W, RL>()),
                          dim3(kQbThreads), 0, c.st, c.rec, c.nsteps, c.skipb[b], c.Qb[b]);
-    else if (W == 64 && c.P < qb2)
+    else if (W == 64 && c.P < 16)
       hipLaunchKernelGGL((qbuild_kernel<T, W, 2>), dim3(c.P, qbuild_blocks<W, 2>()),
                          dim3(kQbThreads), 0, c.st, c.rec, c.nsteps, c.skipb[b], c.Qb[b]);
     else
