@@ -378,3 +378,29 @@ def test_native_issue_rules_match_python(monkeypatch):
                             want_m = choose_merged(world, k, want_q)
                             assert (bool(q.value), bool(mg.value)) == (want_q, want_m), \
                                 (world, dt, W, mma, k, mode)
+
+
+def test_quad_and_merge_rules_pin_the_measured_choices():
+    """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
+    quad steps on 1, 2 and 4 GPUs (64 / 32 / 16 pairs per chain step, 16384
+    rows) but not on 8 (8 pairs); 4096^2 on one GPU does not (16 pairs on
+    4096-row columns); 8192^2 on one GPU does, merged (32 pairs)."""
+    import torch
+
+    from svdj.models.block import resolve_quad
+    from svdj.parallel.distributed import choose_merged
+
+    def plan(n, P, m=None):
+        m_pad = m or n
+        k = n // (2 * P) // 64  # W-blocks per super-block
+        q = resolve_quad("auto", torch.float32, 64, "bf16x6", k, P, m_pad)
+        return q, choose_merged(P, k, q)
+
+    assert plan(16384, 1) == (True, True)
+    assert plan(16384, 2) == (True, False)
+    assert plan(16384, 4) == (True, False)
+    assert plan(16384, 8) == (False, False)
+    assert plan(4096, 1) == (False, False)
+    assert plan(8192, 1) == (True, True)
+    assert plan(32768, 8) == (True, False)
+    assert not resolve_quad("auto", torch.float64, 64, "native", 128, 1, 16384)
