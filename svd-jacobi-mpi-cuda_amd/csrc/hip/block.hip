@@ -1981,13 +1981,20 @@ __global__ __launch_bounds__(kUpdThreads) void quad_update_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* Rg = T1 + (size_t)(j == 0 ? 2 * q + 1 : 2 * q) * N * N + W + 32 * oj;
   const double* Lg = T1 + (size_t)(j == 0 ? 2 * q : 2 * q + 1) * N * N;
-  for (int idx = tid; idx < N * 32; idx += kUpdThreads) {
-    const int r = idx >> 5, cc = idx & 31;
-    Rs[r * HP + cc] = (float)Rg[(size_t)r * N + cc];
+  // 16-byte loads, all issued before the first use (latency-bound otherwise)
+#pragma unroll
+  for (int u = 0; u < N * 32 / 2 / kUpdThreads; ++u) {
+    const int idx = u * kUpdThreads + tid, r = idx >> 4, cc = (idx & 15) * 2;
+    const double2 v = *reinterpret_cast<const double2*>(Rg + (size_t)r * N + cc);
+    Rs[r * HP + cc] = (float)v.x;
+    Rs[r * HP + cc + 1] = (float)v.y;
   }
-  for (int idx = tid; idx < N * W; idx += kUpdThreads) {
-    const int r = idx >> 6, cc = idx & 63;
-    Ls[r * (W + 4) + cc] = (float)Lg[(size_t)r * N + cc];
+#pragma unroll
+  for (int u = 0; u < N * W / 2 / kUpdThreads; ++u) {
+    const int idx = u * kUpdThreads + tid, r = idx >> 5, cc = (idx & 31) * 2;
+    const double2 v = *reinterpret_cast<const double2*>(Lg + (size_t)r * N + cc);
+    Ls[r * (W + 4) + cc] = (float)v.x;
+    Ls[r * (W + 4) + cc + 1] = (float)v.y;
   }
   // slabs of quad q: r = 0 (a,d), 1 (b,c), 2 (a,b), 3 (c,d), gch chunks each
   // (16-byte loads, four independent sums per thread and four slabs' worth in
