@@ -21,9 +21,10 @@
 extern "C" {
 #endif
 
-// Communicator bootstrap through a file: rank 0 creates the RCCL unique id
-// and publishes it at `id_path` (atomic rename); the other ranks wait for it
-// (up to timeout_s).  The caller has selected the rank's device first.
+// Communicator bootstrap through a file (the role of the reference's
+// MPI_Init / MPI_Comm_rank, main.cu:1680-1694): rank 0 creates the RCCL
+// unique id and publishes it at `id_path` (atomic rename); the other ranks
+// wait for it (up to timeout_s).  The caller has selected the rank's device first.
 // *comm receives an ncclComm_t.  Returns 0 or <0.
 int svdj_dist_comm_init(int rank, int world, const char* id_path, double timeout_s, void** comm);
 // Its host part (no RCCL): rank 0 publishes the n-byte id (n = sizeof

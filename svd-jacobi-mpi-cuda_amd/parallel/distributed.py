@@ -49,7 +49,10 @@ from .schedule import distributed_sweep_plan, tournament
 def choose_merged(P: int, k: int, quad: bool) -> bool:
     """One-GPU merged issue (PipelineExecutor.run_merged) for k W-blocks per
     super-block: from 64 pairs per chain step, 32 with quad steps (measured:
-    see the comment at its use in DistributedBlockJacobi._solve).
+    see the comment at its use in DistributedBlockJacobi._solve).  The
+    reference's single-process path rotates one pair per launch
+    (main.cu:727-758); this is the opposite end: all of a step's pairs of
+    both chains in one launch.
     SVDJ_MERGE_CHAINS=0/1 overrides.  libsvdj_dist: svdj_dist_issue_rules."""
     env = os.environ.get("SVDJ_MERGE_CHAINS")
     if env is not None:
