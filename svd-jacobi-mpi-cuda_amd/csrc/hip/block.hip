@@ -2121,7 +2121,12 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
 
-template <int NP>
+// ABL (tools/micro/quad_apply_ab.hip only; production launches ABL = 0):
+// bit 0 one MFMA per k block instead of 1 + (products of order < NP), B
+// fragments still read; bit 1 no global memory (no DMA, no waits, no
+// stores); bit 2 no MFMA loop at all (split, barrier, epilogue, DMA only);
+// bit 3 never the cheap (first-order) k-block form.
+template <int NP, int ABL = 0>
 __global__ __launch_bounds__(kQuadTsThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
                      int v_tiles, const int32_t* __restrict__ pairs, int nq,
@@ -2167,6 +2172,28 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
 #pragma unroll
         for (int p = 0; p < NP; ++p) qf[kb][p] = tp[(kb * 8 * NP + p) * SVDJ_WAVE];
     }
+    // Halves of the k range (k blocks 0-7 = blocks a, b of the quad, 8-15 =
+    // c, d) whose slice of T - I is below 2^-9 in magnitude: there the
+    // order-2 products (q0 x2, q1 x1, q2 x0 <= 3 2^-18 |t||x| <= 3 2^-27 |x|,
+    // below the fp32 rounding of the output) are dropped, 3 MFMAs per k block
+    // instead of 6.  With T = T1 T2 (pairs (a,c), (b,d) then (a,d), (b,c)),
+    // for an output column in a or b the rows of a and b are second order in
+    // the rotation angles (T_aa - I, T_ba = T1_bd T2_da), those of c and d
+    // first order; for c or d the other way round -- so once the angles are
+    // below ~0.04 one half of every column tile takes the cheap form.
+    uint32_t cheap = 0;
+    if constexpr (NP == 3 && (ABL & 8) == 0) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float mx = 0.0f;
+#pragma unroll
+        for (int kb = 8 * hf; kb < 8 * hf + 8; ++kb)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf((float)qf[kb][0][e]));
+        if (wave_max(mx) <= 0.001953125f) cheap |= 1u << hf;
+      }
+      cheap = __builtin_amdgcn_readfirstlane(cheap);
+    }
     // this wave's 32 columns: block wave >> 1 of [a b c d], half wave & 1
     const int32_t* qp = pairs + 4 * q;
     const int qb = wave >> 1;
@@ -2175,6 +2202,7 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
     float* const ownV = V ? V + (size_t)col0 * ldv : nullptr;
 
     auto dma = [&](int t, int buf) {  // raw tile t, own 32 columns -> R[buf] (4 x 1 KB)
+      if constexpr ((ABL & 2) != 0) return;
       const bool isA = t < a_tiles;
       const float* base = isA ? ownA : ownV;
       const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
@@ -2184,11 +2212,13 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
         __builtin_amdgcn_global_load_lds(base + (size_t)(8 * i + (lane >> 3)) * ld + r0 + (lane & 7) * 4,
                                          dst + i * 1024, 16, 0, 0);
     };
-    auto tile = [&](int t, auto bufc) {
+    auto tile = [&](int t, auto bufc, auto chc) {
       constexpr int buf = decltype(bufc)::value;
+      constexpr int CH = decltype(chc)::value;  // cheap halves (bit 0: k blocks 0-7, bit 1: 8-15)
       // 1. own DMA of tile t landed (younger: stores of t-1, DMA of t+1)
       const int younger = (t > t0 ? 16 : 0) + (t + 1 < t1 ? 4 : 0);
-      if (younger == 20) wait_vmcnt<20>();
+      if constexpr ((ABL & 2) != 0) (void)younger;
+      else if (younger == 20) wait_vmcnt<20>();
       else if (younger == 16) wait_vmcnt<16>();
       else if (younger == 4) wait_vmcnt<4>();
       else wait_vmcnt<0>();
@@ -2212,16 +2242,52 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // 3. 16 k blocks x (1 + 5) MFMAs against the register-resident slice
+      // 3. 16 k blocks x (1 + 5) MFMAs (1 + 2 in a cheap half) against the
+      //    register-resident slice
       const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
       f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
+      // k blocks [k0, k0 + 8): first-order products only (cheap half) or all
+      // products of order < NP
+      auto khalf = [&](auto k0c) {
+        constexpr int k0 = decltype(k0c)::value;
+        if constexpr (NP == 3 && ((CH >> (k0 / 8)) & 1) != 0) {
 #pragma unroll
-      for (int kb = 0; kb < 16; ++kb) {
+          for (int kb = k0; kb < k0 + 8; ++kb) {
+            const bf16x8 x0 = Sr[(kb * NP + 0) * SVDJ_WAVE], x1 = Sr[(kb * NP + 1) * SVDJ_WAVE];
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], x1, lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][1], x0, lo, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], x0, acc, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int kb = k0; kb < k0 + 8; ++kb) {
+            bf16x8 xs[NP];
+#pragma unroll
+            for (int i = 0; i < NP; ++i) xs[i] = Sr[(kb * NP + i) * SVDJ_WAVE];
+            lo = mfma_split<NP, 1>(qf[kb], xs, lo);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+          }
+        }
+      };
+      if constexpr ((ABL & 5) == 0) {
+        khalf(std::integral_constant<int, 0>{});
+        khalf(std::integral_constant<int, 8>{});
+      }
+#pragma unroll
+      for (int kb = 0; kb < 16 && (ABL & 5) == 1; ++kb) {
         bf16x8 xs[NP];
 #pragma unroll
         for (int i = 0; i < NP; ++i) xs[i] = Sr[(kb * NP + i) * SVDJ_WAVE];
-        lo = mfma_split<NP, 1>(qf[kb], xs, lo);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+        if constexpr ((ABL & 1) != 0) {
+          using i32x4 = __attribute__((ext_vector_type(4))) int;
+          i32x4 x = __builtin_bit_cast(i32x4, xs[0]);
+#pragma unroll
+          for (int i = 1; i < NP; ++i) x ^= __builtin_bit_cast(i32x4, xs[i]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], __builtin_bit_cast(bf16x8, x), acc, 0, 0, 0);
+        } else {
+          lo = mfma_split<NP, 1>(qf[kb], xs, lo);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+        }
       }
       acc += lo;
       // 4. own raw values, still in this wave's raw image R[buf] (its refill,
@@ -2239,8 +2305,11 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = Rr[(8 * g + 4 * h + i) * 32 + c];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            at_u32(own + (size_t)Mfma<float>::acc_row_uni(4 * g + i) * ld, st_off) = v[i] + acc[4 * g + i];
+          for (int i = 0; i < 4; ++i) {
+            const float y = v[i] + acc[4 * g + i];
+            if ((ABL & 2) == 0 || y == -1.2345e-30f)
+              at_u32(own + (size_t)Mfma<float>::acc_row_uni(4 * g + i) * ld, st_off) = y;
+          }
         }
       }
       // 5. tile t + 2 into the raw image this wave just consumed
@@ -2248,9 +2317,19 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
     };
     if (t0 < t1) dma(t0, 0);
     if (t0 + 1 < t1) dma(t0 + 1, 1);
-    for (int t = t0; t < t1; t += 2) {
-      tile(t, std::integral_constant<int, 0>{});
-      if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
+    // the tile loop specialised per cheap-half mask (a branch per k half
+    // inside one loop made the compiler spill the T slice)
+    auto run = [&](auto chc) {
+      for (int t = t0; t < t1; t += 2) {
+        tile(t, std::integral_constant<int, 0>{}, chc);
+        if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{}, chc);
+      }
+    };
+    if (cheap == 0) run(std::integral_constant<int, 0>{});
+    else if constexpr (NP == 3) {
+      if (cheap == 1) run(std::integral_constant<int, 1>{});
+      else if (cheap == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
     }
     // the next item re-stages both images
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
