@@ -109,15 +109,16 @@ DRIVER_BIN = PKG / "bin" / "svdj_main"
 
 def build_driver(force: bool = False, verbose: bool = False) -> Path:
     """Native single-GPU driver (reference `SVD_Jacobi_MPI_CUDA <n>` parity),
-    linked against the two in-tree libraries with an $ORIGIN rpath."""
-    cpu, hip = build_cpu(force, verbose), build_hip(force, verbose)
+    linked against the in-tree libraries with an $ORIGIN rpath (its default
+    block engine is libsvdj_dist's plan at world 1, no RCCL communicator)."""
+    cpu, hip, dist = build_cpu(force, verbose), build_hip(force, verbose), build_dist(force, verbose)
     DRIVER_BIN.parent.mkdir(exist_ok=True)
-    if not force and not _stale(DRIVER_BIN, [DRIVER_SRC, cpu, hip] + HEADERS):
+    if not force and not _stale(DRIVER_BIN, [DRIVER_SRC, cpu, hip, dist] + HEADERS):
         return DRIVER_BIN
     tmp = DRIVER_BIN.with_suffix(".tmp")
     _run([_hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", f"-I{CSRC / 'include'}",
-          DRIVER_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_hip", "-lsvdj_cpu",
-          "-Wl,-rpath,$ORIGIN/../lib"], verbose)
+          DRIVER_SRC, "-o", tmp, f"-L{LIBDIR}", "-lsvdj_dist", "-lsvdj_hip", "-lsvdj_cpu",
+          "-lrccl", "-Wl,-rpath,$ORIGIN/../lib"], verbose)
     os.replace(tmp, DRIVER_BIN)
     return DRIVER_BIN
 

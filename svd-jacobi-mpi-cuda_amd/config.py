@@ -37,6 +37,19 @@ class SVDOptions(enum.IntEnum):
         return table[s]
 
 
+def debug_knob(key: str, default=None):
+    """Value of ``key`` in the A/B switch SVDJ_DEBUG="key=value,..." (int),
+    or ``default`` -- the Python twin of csrc/include/svdj_debug.h, which
+    lists the keys.  Production runs never set it."""
+    import os
+
+    for item in os.environ.get("SVDJ_DEBUG", "").split(","):
+        k, sep, v = item.partition("=")
+        if sep and k.strip() == key:
+            return int(v)
+    return default
+
+
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "fp64": torch.float64,
            "float64": torch.float64, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
 

@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "svdj_cpu.h"
+#include "svdj_debug.h"
 #include "svdj_hip.h"
 
 namespace {
@@ -105,10 +106,11 @@ extern "C" const char* svdj_dist_last_error(void) { return g_err; }
 // sets a fresh one before forking) or torchrun's TORCHELASTIC_RUN_ID joined
 // with TORCHELASTIC_RESTART_COUNT (an elastic restart, or a reused
 // --rdzv-id after a crash, must not pick up the dead attempt's id).  The
-// file's age is checked in every case: with a token it must be younger than
-// timeout_s (a leftover of an older job with the same token is refused),
-// without one younger than 30 s (tokenless launchers start their ranks
-// together and remove the file before their rendezvous, as bench.py does).
+// file's age is checked in every case, against the start of the reading
+// process: with a token it must be younger than that minus timeout_s (a
+// leftover of an older job with the same token is refused), without one
+// than that minus 30 s (tokenless launchers start their ranks together and
+// remove the file before their rendezvous, as bench.py does).
 namespace {
 struct IdFile {
   char magic[8];
@@ -127,6 +129,39 @@ std::string job_token() {
   return std::string();
 }
 }  // namespace
+
+// Wall-clock start of this process (Linux /proc), or now if unavailable.
+static time_t process_start_time() {
+  static const time_t t = [] {
+    const time_t now = time(nullptr);
+    long long btime = -1;
+    if (FILE* f = fopen("/proc/stat", "r")) {
+      char line[256];
+      while (fgets(line, sizeof(line), f))
+        if (!strncmp(line, "btime ", 6)) btime = atoll(line + 6);
+      fclose(f);
+    }
+    unsigned long long start_ticks = 0;
+    bool ok = false;
+    if (FILE* f = fopen("/proc/self/stat", "r")) {
+      char buf[1024];
+      const size_t k = fread(buf, 1, sizeof(buf) - 1, f);
+      fclose(f);
+      buf[k] = 0;
+      // field 22 (starttime) counts from the field after the ')' of comm
+      if (const char* p = strrchr(buf, ')')) {
+        int field = 2;
+        for (const char* q = p + 1; *q && !ok; ++q)
+          if (*q == ' ' && ++field == 22) ok = sscanf(q + 1, "%llu", &start_ticks) == 1;
+      }
+    }
+    const long hz = sysconf(_SC_CLK_TCK);
+    if (btime < 0 || !ok || hz <= 0) return now;
+    const time_t s = (time_t)(btime + (long long)(start_ticks / (unsigned long long)hz));
+    return s <= now ? s : now;
+  }();
+  return t;
+}
 
 // Host part of the bootstrap (no RCCL, no GPU; CPU-tested under ASan):
 // rank 0 publishes `n` bytes at `path` (written to path.tmp, then renamed),
@@ -150,8 +185,12 @@ extern "C" int svdj_dist_id_file(int rank, const char* id_path, double timeout_s
     if (rename(tmp.c_str(), path.c_str()) != 0) return fail(-1, "cannot publish %s", path.c_str());
     return 0;
   }
+  // freshness is measured from this process's start, not from this call: the
+  // ranks of one launch start together, and a peer that reaches here late
+  // (slow GPU init or data load) must still accept the file its rank 0
+  // published after the launch
   const double window = token.empty() ? 30.0 : (timeout_s > 30 ? timeout_s : 30.0);
-  const time_t not_before = time(nullptr) - (time_t)window;
+  const time_t not_before = process_start_time() - (time_t)window;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     struct stat sb;
@@ -636,8 +675,8 @@ extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k
     return fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
   const int hk = k / 2;
   *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && (hk >= 32 || (hk >= 16 && m_pad >= 16384))));
-  const char* em = getenv("SVDJ_MERGE_CHAINS");
-  *merged = world == 1 && (em ? atoi(em) == 1 : hk >= (*quad ? 32 : 64));
+  const int force = svdj_debug_knob("merge", -1);  // A/B only (svdj_debug.h), world 1 only
+  *merged = world == 1 && (force >= 0 ? force == 1 : hk >= (*quad ? 32 : 64));
   return 0;
 }
 
@@ -763,13 +802,37 @@ int exchange_ops(const Tour& tour, int round, int g, const XMsg* msgs, int nm, b
   return 0;
 }
 
+// Wait for stream s without blocking forever.  Handle creation runs before
+// the solve's watchdog exists, so its collectives are polled here: an RCCL
+// async error or timeout_s without completion aborts the communicator (the
+// RCCL kernels spinning on a dead peer are released and the stream drains)
+// and returns -300, as a watchdog abort in svdj_dist_solve does.
+int poll_stream(hipStream_t s, ncclComm_t comm, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return fail(-100, "stream error: %s", hipGetErrorString(q));
+    ncclResult_t ae = ncclSuccess;
+    const ncclResult_t r = ncclCommGetAsyncError(comm, &ae);
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (r != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress) || el > timeout_s) {
+      (void)ncclCommAbort(comm);
+      (void)hipStreamSynchronize(s);
+      return fail(-300, "handle creation: %s; communicator aborted",
+                  el > timeout_s ? "collective timed out" : "RCCL async error");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 // Exchange calibration (pipeline.calibrate_exchange, ADVICE r3 / VERDICT r4):
 // at handle creation, from 4 ranks with exchange auto, one half exchange of
 // the first tournament round is timed both ways on this job's links (real
 // half-buffer sizes of A, the norms and V; one warm-up, the best of 3; every
 // timing the max over ranks), and spread is kept only if it is >= 10 %
 // faster.  Every rank takes the same decision (the times are all-reduced).
-int calibrate_exchange(svdj_dist_handle_t* h) {
+int calibrate_exchange(svdj_dist_handle_t* h, double timeout_s) {
   const int P = h->world, g = h->rank;
   Tour tour(P);
   const size_t es = h->es;
@@ -793,23 +856,23 @@ int calibrate_exchange(svdj_dist_handle_t* h) {
     if (n[2]) msgs[nm++] = {buf[2][0], buf[2][1], n[2], spread ? (char*)h->relay[1] : nullptr, h->relay_n[1]};
     for (int it = 0; it < 4 && !rc; ++it) {
       // line the ranks up (a tiny all-reduce), then time one exchange
-      if (ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess ||
-          hipStreamSynchronize(h->sc) != hipSuccess) {
+      if (ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess) {
         rc = fail(-200, "calibration barrier failed");
         break;
       }
+      if ((rc = poll_stream(h->sc, h->comm, timeout_s))) break;
       const auto t0 = std::chrono::steady_clock::now();
       if ((rc = exchange_ops(tour, 1, g, msgs, nm, spread, nt, es, h->comm, h->sc))) break;
-      if (hipStreamSynchronize(h->sc) != hipSuccess) {
-        rc = fail(-100, "calibration sync failed");
-        break;
-      }
+      if ((rc = poll_stream(h->sc, h->comm, timeout_s))) break;
       double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (hipMemcpy(dt, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
-          ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess ||
-          hipStreamSynchronize(h->sc) != hipSuccess ||
-          hipMemcpy(&t, dt, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) {
+          ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, h->comm, h->sc) != ncclSuccess) {
         rc = fail(-200, "calibration max over ranks failed");
+        break;
+      }
+      if ((rc = poll_stream(h->sc, h->comm, timeout_s))) break;
+      if (hipMemcpy(&t, dt, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) {
+        rc = fail(-100, "calibration copy failed");
         break;
       }
       if (it) best[v] = std::min(best[v], t);
@@ -886,7 +949,29 @@ extern "C" int svdj_dist_handle_create(const svdj_dist_problem* p, void** out) {
     else
       h->own_sc = true;
   }
-  if (!rc && h->world >= 4 && p->exchange == 0) guard(calibrate_exchange(h));
+  // Measured exchange choice: a collective, so first a go/no-go over ALL
+  // ranks (max of the local failure flags; a rank that failed above still
+  // takes part), then every rank calibrates or every rank gives up -- a rank
+  // that skipped calibration alone would leave its peers blocked in it.
+  if (h->world >= 4 && p->exchange == 0 && h->sc) {
+    const double tmo = p->timeout_s > 0 ? p->timeout_s : 600.0;
+    int32_t* flag = nullptr;
+    int32_t any = rc ? 1 : 0;
+    if (hipMalloc((void**)&flag, sizeof(int32_t)) != hipSuccess ||
+        hipMemcpy(flag, &any, sizeof(any), hipMemcpyHostToDevice) != hipSuccess) {
+      rc = rc ? rc : fail(-100, "go/no-go flag: hipMalloc failed");
+    } else if (ncclAllReduce(flag, flag, 1, ncclInt32, ncclMax, h->comm, h->sc) != ncclSuccess) {
+      rc = rc ? rc : fail(-200, "go/no-go all-reduce failed");
+    } else if (int r = poll_stream(h->sc, h->comm, tmo)) {
+      rc = rc ? rc : r;
+    } else if (hipMemcpy(&any, flag, sizeof(any), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = rc ? rc : fail(-100, "go/no-go flag copy failed");
+    } else if (any && !rc) {
+      rc = fail(-2, "handle creation failed on another rank: exchange calibration skipped");
+    }
+    (void)hipFree(flag);
+    if (!rc) guard(calibrate_exchange(h, tmo));
+  }
   if (rc) {
     handle_free(h);
     return rc;
@@ -1173,10 +1258,12 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
       {
         std::lock_guard<std::mutex> lk(wd.mu);
         if (wd.fired.load()) return fail(-300, "%s", wd.why);
-        NCCLC(ncclAllReduce(h->metric, h->metric, 1, ncclUint32, ncclMax, comm, sa));
-        NCCLC(ncclAllReduce(h->metric + 1, h->metric + 1, 1, ncclUint32, ncclSum, comm, sa));
-        NCCLC(ncclAllReduce(h->metric + 4, h->metric + 4, 1, ncclUint32, ncclMax, comm, sa));
-        NCCLC(ncclAllReduce(h->metric + 5, h->metric + 5, 1, ncclUint32, ncclSum, comm, sa));
+        if (P > 1) {  // one GPU (comm may be NULL): the local words are the global ones
+          NCCLC(ncclAllReduce(h->metric, h->metric, 1, ncclUint32, ncclMax, comm, sa));
+          NCCLC(ncclAllReduce(h->metric + 1, h->metric + 1, 1, ncclUint32, ncclSum, comm, sa));
+          NCCLC(ncclAllReduce(h->metric + 4, h->metric + 4, 1, ncclUint32, ncclMax, comm, sa));
+          NCCLC(ncclAllReduce(h->metric + 5, h->metric + 5, 1, ncclUint32, ncclSum, comm, sa));
+        }
       }
       HIPC(hipMemcpyAsync(hm, h->metric, sizeof(hm), hipMemcpyDeviceToHost, sa));
       return wait_sa();

@@ -23,6 +23,7 @@
 // full Gram, which re-measures every within-block angle from the data.
 #include "common.hpp"
 #include "evd_deal_tables.hpp"
+#include "svdj_debug.h"
 #include "svdj_hip.h"
 #include "svdj_stop.h"
 
@@ -2502,10 +2503,7 @@ static void quad_geometry(Geometry& g, int P, int m_pad, int n_v) {
   // 874-884, 8 chunks 933 (profiles/r5_gram)
   const int nq = P / 2 > 0 ? P / 2 : 1;
   int want = nq >= 32 ? 4 : (256 + nq - 1) / nq;
-  static const int forced = [] {  // A/B measurements only
-    const char* e = getenv("SVDJ_QUAD_GRAM_CHUNKS");
-    return e ? atoi(e) : 0;
-  }();
+  static const int forced = svdj_debug_knob("quad_gram_chunks", 0);  // A/B only (svdj_debug.h)
   if (forced > 0) want = forced;
   const int maxc = m_pad / 128;
   g.qgch = want < 1 ? 1 : (want > maxc ? maxc : want);
@@ -2536,11 +2534,10 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
   // rows (512 workgroups) vs 325 at 512 (1024 workgroups).  The EVD sums one
   // slab per chunk, so short chunks put more slab data on its critical path.
   int want = P >= 32 ? (256 + P - 1) / P : min((m_pad + 511) / 512, (512 + P - 1) / P);
-  if (P >= 64 && want < 4) want = 4;
-  static const int forced = [] {  // A/B measurements only
-    const char* e = getenv("SVDJ_GRAM_CHUNKS");
-    return e ? atoi(e) : 0;
-  }();
+  // (the bump applies to the split-bf16 launches it was measured on: merged
+  // fp32 one-GPU steps of 128 pairs; fp64 steps keep the target rule)
+  if (mma != 0 && P >= 64 && want < 4) want = 4;
+  static const int forced = svdj_debug_knob("gram_chunks", 0);  // A/B only (svdj_debug.h)
   if (forced > 0) want = forced;
   int maxc = m_pad / 128;
   g.gchunks = want < 1 ? 1 : (want > maxc ? maxc : want);
@@ -2596,7 +2593,11 @@ static bool has_quad_steps(const int32_t* modes, int steps) {
   return false;
 }
 static size_t ws_bytes_for(int esize, int W, int P, int m_pad, bool quad) {
-  Geometry g = make_geometry(W, P, m_pad, 0);
+  // the Gram chunking depends on the apply mode (split-bf16 launches may take
+  // more chunks): size the slabs for the larger of the two
+  Geometry g = make_geometry(W, P, m_pad, 0, 0);
+  const Geometry gs = make_geometry(W, P, m_pad, 0, 1);
+  if (gs.gchunks > g.gchunks) g = gs;
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
@@ -2780,17 +2781,13 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
 
 // Gram + EVD of step s (Q and the skip flags are double-buffered so evd(s+1)
 // never overwrites what apply(s) may still read).
-// Dispatch order of the row chunks (SVDJ_STREAM_ORDER, bit 0: cross Gram
-// chunks last-first, bit 1: the apply's V chunks before A's).
+// Dispatch order of the row chunks (SVDJ_DEBUG stream_order, bit 0: cross
+// Gram chunks last-first, bit 1: the apply's V chunks before A's).
 // Default 2: V first, so A -- which the next step's Gram reads -- holds the
 // most recently written lines (single-stream 16384^2 step 642 -> 614 us,
 // bitwise the same result; neutral with two concurrent chains).
 static int stream_order() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SVDJ_STREAM_ORDER");
-    v = e ? atoi(e) : 2;
-  }
+  static const int v = svdj_debug_knob("stream_order", 2);
   return v;
 }
 

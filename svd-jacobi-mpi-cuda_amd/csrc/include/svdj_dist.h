@@ -117,7 +117,11 @@ typedef struct {
 // metric, every device pair list of the plan (for each placement of the
 // halves), events and the comm stream -- allocated once, so a solve
 // allocates nothing.  Reads rank, world, comm, dtype, W, m_pad, n_v, B,
-// Vt (NULL or not), the streams and comm_timing from *p.
+// Vt (NULL or not), the streams and comm_timing from *p.  On one GPU comm may
+// be NULL (no RCCL call is made at world 1).  From 4 ranks with exchange auto
+// it is collective (go/no-go flag, then the exchange calibration, both
+// polled against timeout_s); -300: a peer died or hung and the communicator
+// was aborted -- it must not be destroyed.
 int svdj_dist_handle_create(const svdj_dist_problem* p, void** handle);
 int svdj_dist_handle_destroy(void* handle);
 
@@ -139,7 +143,7 @@ int svdj_dist_plan(int world, int rank, int32_t* out, int cap);
 // step, or 16 on columns of >= 16384 rows; fp32 W = 64 split-bf16 apply,
 // k % 4 == 0) and, on one GPU, the
 // merged issue (from 64 pairs per chain step, 32 with quad steps;
-// SVDJ_MERGE_CHAINS=0/1 overrides) -- models/block.py choose_quad and
+// SVDJ_DEBUG merge=0/1 overrides, svdj_debug.h) -- models/block.py choose_quad and
 // parallel/distributed.py choose_merged.  Returns 0 or <0.
 int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k, int m_pad, int quad_mode,
                           int* quad, int* merged);

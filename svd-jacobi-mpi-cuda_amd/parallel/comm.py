@@ -94,6 +94,20 @@ class Communicator:
         self.rank = dist.get_rank() if dist.is_initialized() else rank
         self.world = dist.get_world_size() if dist.is_initialized() else world
 
+    @classmethod
+    def local(cls, device) -> "Communicator":
+        """A world-1 communicator on ``device`` that never touches a process
+        group, even inside a distributed job: the single-GPU solve behind
+        ``api.svd`` runs the distributed engine's plan at P = 1 (no
+        exchanges, every collective the identity)."""
+        c = cls.__new__(cls)
+        c.device = torch.device(device)
+        c.backend = "nccl" if c.device.type == "cuda" else "gloo"
+        c.timeout_s = default_timeout_s()
+        c.owns_group = False
+        c.rank, c.world = 0, 1
+        return c
+
     @property
     def distributed(self) -> bool:
         return self.world > 1
@@ -204,8 +218,10 @@ class Communicator:
         if self.distributed:
             a = t[0:2].clone()
             b = t[2:4].clone()
+            self._host_sync()  # gloo reads device tensors outside stream order
             dist.all_reduce(a, op=dist.ReduceOp.MAX)
             dist.all_reduce(b, op=dist.ReduceOp.SUM)
+            self._host_sync()
             t = torch.cat([a, b])
         h = t.cpu()
         return float(h[0]), float(h[1]), float(h[2]), float(h[3])
@@ -218,15 +234,31 @@ class Communicator:
             self._host_sync()
         return t
 
-    def ordered_sum_(self, t: torch.Tensor) -> torch.Tensor:
+    # temporary bytes ordered_sum_ may hold at once (world x slab)
+    ORDERED_SUM_BYTES = 256 << 20
+
+    def ordered_sum_(self, t: torch.Tensor, max_bytes: int | None = None) -> torch.Tensor:
         """In-place sum over ranks added in rank order, t_0 + t_1 + ..., on
         every rank (all-gather, then local adds): bitwise the same result on
-        any backend and ring, unlike a floating all-reduce."""
-        if self.distributed:
-            parts = self.allgather(t)
-            t.copy_(parts[0])
+        any backend and ring, unlike a floating all-reduce.  The all-gather
+        runs over slabs of t's flat view so that at most ``max_bytes``
+        (default ORDERED_SUM_BYTES) of gathered copies exist at once: a whole
+        n x n Gram gathered from P ranks would need P n^2 elements (n = 65536
+        fp64 at P = 8: 256 GB).  Slabbing does not change any element's
+        additions, so the result is the same bits."""
+        if not self.distributed:
+            return t
+        cap = self.ORDERED_SUM_BYTES if max_bytes is None else int(max_bytes)
+        flat = t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
+        per = max(1, cap // max(1, self.world * flat.element_size()))
+        for s0 in range(0, flat.numel(), per):
+            sl = flat[s0:s0 + per]
+            parts = self.allgather(sl)
+            sl.copy_(parts[0])
             for h in range(1, self.world):
-                t.add_(parts[h])
+                sl.add_(parts[h])
+        if not t.is_contiguous():
+            t.copy_(flat.view_as(t))
         return t
 
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
@@ -259,7 +291,9 @@ class Communicator:
         if not self.distributed:
             return float(x)
         t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self._host_sync()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self._host_sync()
         return float(t.cpu()[0])
 
     def destroy(self):

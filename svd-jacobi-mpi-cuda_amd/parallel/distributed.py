@@ -33,7 +33,7 @@ import time
 
 import torch
 
-from ..config import SolverConfig, SVDOptions
+from ..config import SolverConfig, SVDOptions, debug_knob
 from ..models.base import SVDResult, Solver
 from ..models import precondition as pre
 from ..models.block import choose_block, choose_mma, resolve_inner_order, resolve_quad
@@ -53,11 +53,14 @@ def choose_merged(P: int, k: int, quad: bool) -> bool:
     reference's single-process path rotates one pair per launch
     (main.cu:727-758); this is the opposite end: all of a step's pairs of
     both chains in one launch.
-    SVDJ_MERGE_CHAINS=0/1 overrides.  libsvdj_dist: svdj_dist_issue_rules."""
-    env = os.environ.get("SVDJ_MERGE_CHAINS")
-    if env is not None:
-        return env == "1"
-    return P == 1 and k // 2 >= (32 if quad else 64)
+    On one GPU only, in both engines; SVDJ_DEBUG merge=0/1 overrides there
+    (config.debug_knob).  libsvdj_dist: svdj_dist_issue_rules."""
+    if P != 1:
+        return False
+    force = debug_knob("merge")
+    if force is not None:
+        return force == 1
+    return k // 2 >= (32 if quad else 64)
 
 
 class DistributedBlockJacobi(Solver):
@@ -327,7 +330,7 @@ class DistributedBlockJacobi(Solver):
         # two-chain solve, the Gram keeps the chunking).  Single steps of 32
         # pairs keep the overlapped chains (8192^2 merged +10 %); quad steps
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
-        # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_MERGE_CHAINS=0/1
+        # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_DEBUG merge=0/1
         # overrides; with exchanges merging was slower at every P.
         merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
                                                                     k, quad)
@@ -410,16 +413,19 @@ class DistributedBlockJacobi(Solver):
             import os
             os._exit(17)
 
+    _STREAMS: dict = {}  # device -> the two chain streams, shared by every solver in the process
+
     def _chain_streams(self, dev):
-        """The chain streams are created ONCE per solver and reused: torch
+        """The chain streams are created ONCE per device and process and
+        reused by every solver (each svd() call builds a new one): torch
         hands out pool streams round robin, and HIP binds each new stream to
         one of GPU_MAX_HW_QUEUES (4) hardware queues, so fresh streams per
-        solve can land on the same queue as each other and serialise."""
+        solve can land on the same queue as each other and serialise.
+        Solves in one process are sequential, so sharing is safe."""
         key = str(dev)
-        cache = self.__dict__.setdefault("_streams", {})
-        if key not in cache:
-            cache[key] = [torch.cuda.Stream(dev) for _ in range(2)]
-        return cache[key]
+        if key not in DistributedBlockJacobi._STREAMS:
+            DistributedBlockJacobi._STREAMS[key] = [torch.cuda.Stream(dev) for _ in range(2)]
+        return DistributedBlockJacobi._STREAMS[key]
 
     # ------------------------------------------------------- data movement
     def _exchange(self, tour, r, phys, At, Vt, D, bufs, B):

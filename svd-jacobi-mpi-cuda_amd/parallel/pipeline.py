@@ -489,7 +489,7 @@ class PipelineExecutor:
     def run(self, plan: SweepPlan, run_steps, phys, merge: bool = False) -> float:
         """Execute one sweep.  ``run_steps(pairs, modes, slot)`` enqueues block
         steps on the current stream; ``merge``: the joint task groups as
-        single launches (SVDJ_MERGE_CHAINS=1 with exchanges; measured slower
+        single launches (the merged issue with exchanges; measured slower
         there).  ``phys`` (per-GPU placement of whole super-blocks) is
         updated after both halves of a round arrived.  Returns host seconds
         spent issuing/blocking on exchanges."""
@@ -545,7 +545,7 @@ class PipelineExecutor:
             if len(tasks) == 2 and merge and list(tasks[0].modes) == list(tasks[1].modes) \
                     and pairs[0].shape == pairs[1].shape:
                 # both tasks as ONE launch per step on the first task's stream,
-                # after the second task's dependencies too (SVDJ_MERGE_CHAINS=1)
+                # after the second task's dependencies too (merged issue)
                 a, b = tasks
                 sa, sb = self.streams[a.stream], self.streams[b.stream]
                 joined = self._event()

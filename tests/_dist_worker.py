@@ -44,6 +44,41 @@ def main():
                 json.dump({"ok_ranks": float(t[0]), "world": comm.world}, f)
         comm.destroy()
         return
+    if mode == "ordsum":  # rank-ordered sum: slabbed (bounded memory) == whole, same bits
+        g = torch.Generator().manual_seed(100 + comm.rank)
+        x = torch.randn(37, 53, generator=g, dtype=torch.float64)
+        whole = comm.ordered_sum_(x.clone(), max_bytes=1 << 30)
+        slab = comm.ordered_sum_(x.clone(), max_bytes=8 * comm.world * 5)  # 5 elements per slab
+        xt = x.clone().t()  # non-contiguous
+        slab_t = comm.ordered_sum_(xt, max_bytes=8 * comm.world * 7)
+        ref = None
+        for h in range(comm.world):
+            y = torch.randn(37, 53, generator=torch.Generator().manual_seed(100 + h),
+                            dtype=torch.float64)
+            ref = y.clone() if ref is None else ref.add_(y)
+        if comm.rank == 0:
+            with open(out, "w") as f:
+                json.dump({"slab_eq_whole": bool(torch.equal(slab, whole)),
+                           "whole_eq_ref": bool(torch.equal(whole, ref)),
+                           "slab_t_eq": bool(torch.equal(slab_t.t(), whole)),
+                           "world": comm.world}, f)
+        comm.destroy()
+        return
+    if mode == "localsvd":  # svd() inside a distributed job solves this rank's matrix alone
+        B = svdj.utils.inputs.random_dense(m, n, dtype=torch.float64, seed=50 + comm.rank)
+        res = svdj.svd(B, method="block", device="cpu", block=W, extra={"engine": "pipeline"})
+        ref = torch.linalg.svdvals(B)
+        err = float((res.S.sort(descending=True).values - ref).abs().max() / ref[0])
+        resid = float((B @ res.V - res.U * res.S).norm() / B.norm())
+        t = torch.tensor([max(err, resid)], dtype=torch.float64)
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if comm.rank == 0:
+            with open(out, "w") as f:
+                json.dump({"max_err": float(t[0]), "engine": res.info["engine"],
+                           "converged": res.converged, "world": comm.world}, f)
+        comm.destroy()
+        return
     if mode == "calib":  # startup exchange calibration: same choice on every rank, data intact
         from svdj.parallel.pipeline import calibrate_exchange
         from svdj.parallel.schedule import tournament

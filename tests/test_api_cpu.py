@@ -215,3 +215,44 @@ def test_norm_floor_relative_to_scale(svdj):
     assert K.norm_floor(torch.float32, 100, 1.0) == 100 * fi.tiny / fi.eps
     assert K.norm_floor(torch.float32, 100, 1e-30) == 100 * fi.tiny  # absolute guard
     assert K.norm_floor(torch.float32, 100, 4.0) == 4 * 100 * fi.tiny / fi.eps
+
+
+@pytest.mark.parametrize("shape,jobs", [((220, 160), ("A", "A")), ((130, 200), ("A", "A")),
+                                        ((200, 128), ("N", "A")), ((200, 128), ("A", "N"))])
+def test_block_engines_agree_cpu(shape, jobs):
+    """svd()'s two single-device engines (models/block.py choose_engine): the
+    pipeline (the distributed plan at P = 1, what a GPU runs by default) and
+    the single-stream round robin give the same factorisation quality, for
+    tall and wide inputs and every job option."""
+    A = svdj.utils.inputs.random_dense(*shape, dtype=torch.float64, seed=21)
+    ref = torch.linalg.svdvals(A)
+    out = {}
+    for eng in ("pipeline", "steps"):
+        r = svdj.svd(A, *jobs, method="block", device="cpu", block=32, extra={"engine": eng})
+        assert r.converged and r.info["engine"] == eng and r.info["block"] == 32
+        assert float((r.S.sort(descending=True).values - ref).abs().max() / ref[0]) < 1e-13
+        if r.U is not None and r.V is not None:
+            assert float((A @ r.V - r.U * r.S).norm() / A.norm()) < 1e-13
+        assert (r.U is None) == (jobs[0] == "N" if shape[0] >= shape[1] else jobs[1] == "N")
+        out[eng] = r
+    assert abs(out["pipeline"].sweeps - out["steps"].sweeps) <= 2
+
+
+def test_block_engine_choice():
+    from svdj.models.block import choose_engine
+
+    cfg = svdj.SolverConfig()
+    assert choose_engine(cfg, torch.device("cuda", 0)) == "pipeline"
+    assert choose_engine(cfg, torch.device("cpu")) == "steps"
+    assert choose_engine(svdj.SolverConfig(extra={"engine": "steps"}), torch.device("cuda", 0)) == "steps"
+    with pytest.raises(ValueError):
+        choose_engine(svdj.SolverConfig(extra={"engine": "fast"}), torch.device("cpu"))
+
+
+def test_local_communicator_is_world_one():
+    from svdj.parallel import Communicator
+
+    c = Communicator.local("cpu")
+    assert (c.rank, c.world, c.distributed) == (0, 1, False)
+    t = torch.arange(6.0)
+    assert torch.equal(c.ordered_sum_(t.clone()), t) and c.max_over_ranks(2.5) == 2.5

@@ -52,6 +52,23 @@ def test_distributed_qr_preconditioned(mode, tmp_path):
 
 
 @pytest.mark.parametrize("world", [2, 3])
+def test_ordered_sum_slabs_are_bitwise_whole(world, tmp_path):
+    """the rank-ordered Gram sum of the distributed QR gathers in
+    slabs of bounded size; the additions per element are unchanged, so the
+    slabbed sum is the same bits as the whole one and as rank-order adds."""
+    rep = _run(world, 10, 10, 32, tmp_path, mode="ordsum")
+    assert rep["slab_eq_whole"] and rep["whole_eq_ref"] and rep["slab_t_eq"], rep
+
+
+def test_svd_inside_distributed_job_is_local(tmp_path):
+    """svd() on a rank of a running job solves that rank's own matrix on a
+    world-1 Communicator.local (it must not join the job's process group)."""
+    rep = _run(2, 150, 128, 32, tmp_path, mode="localsvd")
+    assert rep["engine"] == "pipeline" and rep["converged"], rep
+    assert rep["max_err"] < 1e-12, rep
+
+
+@pytest.mark.parametrize("world", [2, 3])
 def test_local_matrix_distribution_roundtrip(world, tmp_path):
     """Scatter root-owned A to the resident super-blocks and gather it back."""
     rep = _run(world, 130, 100, 32, tmp_path, mode="roundtrip")

@@ -31,6 +31,25 @@ def test_native_driver_block_and_scalar(tmp_path):
     assert any(p.name.startswith("reporte-dimension-256") for p in tmp_path.iterdir())
 
 
+def test_native_driver_engines_agree(tmp_path):
+    """svdj_main's block engines: the default pipeline (libsvdj_dist's plan at
+    world 1, no RCCL communicator: the engine bench.py and svd() run) and the
+    single-stream round robin both verify, in fp32 with W = 64 (split-bf16
+    apply) and fp64, at a size where a chain step holds several pairs."""
+    exe = os.path.join(ROOT, "svd-jacobi-mpi-cuda_amd", "bin", "svdj_main")
+    for dt, lim in (("f32", 2e-4), ("f64", 1e-9)):
+        for eng in ("pipeline", "steps"):
+            r = subprocess.run([exe, "1100", "--m", "1200", "--input", "dense", "--dtype", dt,
+                                "--engine", eng, "--verify", "--no-report"],
+                               capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stdout + r.stderr
+            out = r.stdout
+            assert ("engine: pipeline" in out) == (eng == "pipeline"), out
+            resid = float(out.split("||A-USVt||_F:")[1].split()[0])
+            anorm = 1200 * 1100 / 3.0  # ||U(0,1)||_F^2 ~ mn / 3
+            assert resid / anorm ** 0.5 < lim, out
+
+
 def test_cli_driver_gpu(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "svd_jacobi.py"), "200",
                         "--input", "dense", "--verify", "--report-dir", str(tmp_path),
@@ -145,7 +164,7 @@ def test_merged_issue_is_bitwise_the_two_chain_solve(svdj, cuda, monkeypatch):
     A = torch.rand(16384, 16384, generator=g, device=cuda)
     out = {}
     for merge in ("1", "0"):
-        monkeypatch.setenv("SVDJ_MERGE_CHAINS", merge)
+        monkeypatch.setenv("SVDJ_DEBUG", f"merge={merge}")
         cfg = svdj.SolverConfig(dtype=torch.float32, block=64, max_sweeps=1)
         res = DistributedBlockJacobi(cfg, comm).solve(A)
         assert res.info["merged_chains"] == (merge == "1"), res.info

@@ -179,6 +179,26 @@ def test_svd_quad_end_to_end(svdj, cuda, quad):
     assert rep["orth_u_fro"] < 1.5e-3 and rep["orth_v_fro"] < 2e-4, rep
 
 
+def test_svd_api_runs_the_pipeline_engine(svdj, cuda):
+    """The public entry point gets the headline engine:
+    svdj.svd on a GPU runs the distributed plan at P = 1 -- with 32 pairs per
+    chain step (8192^2: 128 blocks, 2 super-blocks of 64) quad steps and the
+    merged one-GPU issue -- and gives the same result as
+    DistributedBlockJacobi on a world-1 communicator."""
+    from svdj.parallel import Communicator, DistributedBlockJacobi
+    n = 8192
+    A = svdj.utils.inputs.random_dense(n, n, dtype=torch.float32, device=cuda, seed=12)
+    res = svdj.svd(A)
+    assert res.converged and res.info["engine"] == "pipeline", res.info
+    assert res.info["quad"] and res.info["merged_chains"] and res.info["block"] == 64, res.info
+    ref = DistributedBlockJacobi(svdj.SolverConfig(), Communicator.local(cuda)).solve(A)
+    assert ref.sweeps == res.sweeps and torch.equal(ref.S, res.S)
+    rel = float((A @ res.V - res.U * res.S).norm() / A.norm())
+    assert rel < 1e-5, rel
+    steps = svdj.svd(A[:2048, :2048], extra={"engine": "steps"})
+    assert steps.info["engine"] == "steps" and steps.converged
+
+
 def test_svd_quad_without_v_and_bf16(svdj, cuda):
     """Quad steps without V (jobv = NoVec: the apply's V tiles are skipped)
     give bitwise the singular values of the AllVec solve (V never feeds back

@@ -305,6 +305,21 @@ def test_dist_id_file_handshake(tmp_path, monkeypatch):
     os.utime(path.decode(), (old, old))
     assert read(timeout=0.3)[0] == -2
     assert lib.svdj_dist_id_file(1, path, 0.3, ctypes.create_string_buffer(64), 64) == -2  # size
+    # freshness counts from the reading process's start, not from
+    # its call -- a tokenless peer that arrives late (slow GPU init) still
+    # accepts the id its rank 0 published after the launch.  Published 29 s
+    # before this process started: inside the 30 s window of the launch, but
+    # older than 30 s before this call (the test process has run > 1 s).
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID")
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT")
+    publish()
+    import psutil
+    t_start = psutil.Process().create_time()
+    assert time.time() - t_start > 1.0
+    os.utime(path.decode(), (t_start - 29, t_start - 29))
+    assert read(timeout=0.5) == (0, blob)
+    os.utime(path.decode(), (t_start - 40, t_start - 40))  # before the window: a leftover
+    assert read(timeout=0.3)[0] == -2
 
 
 @pytest.mark.parametrize("k,quad", [(8, False), (8, True), (16, True), (128, True)])
@@ -356,29 +371,37 @@ def test_native_issue_rules_match_python(monkeypatch):
     from svdj.ops import _native as nat
     from svdj.parallel.distributed import choose_merged
 
-    monkeypatch.delenv("SVDJ_MERGE_CHAINS", raising=False)
+    import itertools
+
     lib = nat.dist_lib()
     q, mg = ctypes.c_int32(), ctypes.c_int32()
-    for world in (1, 2, 8):
-        for dt, code in ((torch.float32, 0), (torch.float64, 1)):
-            for W in (32, 64):
-                for mma, mcode in (("native", 0), ("bf16x6", 1), ("bf16x3", 2)):
-                    for k, m_pad in ((8, 16384), (16, 8192), (16, 16384), (30, 32768),
-                                     (32, 4096), (32, 16384), (62, 8192), (64, 8192),
-                                     (128, 16384), (256, 65536)):
-                        for mode, mc in (("auto", 0), ("on", 1), ("off", 2)):
-                            rc = lib.svdj_dist_issue_rules(world, code, W, mcode, k, m_pad, mc,
-                                                           ctypes.byref(q), ctypes.byref(mg))
-                            try:
-                                want_q = resolve_quad(mode, dt, W, mma, k, world, m_pad)
-                            except ValueError:
-                                assert rc < 0, (world, dt, W, mma, k, mode)
-                                continue
-                            assert rc == 0, (world, dt, W, mma, k, mode)
-                            want_m = choose_merged(world, k, want_q)
-                            assert (bool(q.value), bool(mg.value)) == (want_q, want_m), \
-                                (world, dt, W, mma, k, mode)
-
+    cases = itertools.product(
+        (1, 2, 8), ((torch.float32, 0), (torch.float64, 1)), (32, 64),
+        (("native", 0), ("bf16x6", 1), ("bf16x3", 2)),
+        ((8, 16384), (16, 8192), (16, 16384), (30, 32768), (32, 4096), (32, 16384), (62, 8192),
+         (64, 8192), (128, 16384), (256, 65536)),
+        (("auto", 0), ("on", 1), ("off", 2)))
+    cases = list(cases)
+    # the A/B override (SVDJ_DEBUG merge=0/1) acts on one GPU only, in both engines
+    for dbg in (None, "merge=0", "merge=1"):
+        if dbg is None:
+            monkeypatch.delenv("SVDJ_DEBUG", raising=False)
+        else:
+            monkeypatch.setenv("SVDJ_DEBUG", dbg)
+        for world, (dt, code), W, (mma, mcode), (k, m_pad), (mode, mc) in cases:
+            where = (dbg, world, dt, W, mma, k, mode)
+            rc = lib.svdj_dist_issue_rules(world, code, W, mcode, k, m_pad, mc,
+                                           ctypes.byref(q), ctypes.byref(mg))
+            try:
+                want_q = resolve_quad(mode, dt, W, mma, k, world, m_pad)
+            except ValueError:
+                assert rc < 0, where
+                continue
+            assert rc == 0, where
+            want_m = choose_merged(world, k, want_q)
+            assert (bool(q.value), bool(mg.value)) == (want_q, want_m), where
+            if world > 1:
+                assert not want_m, where
 
 def test_quad_and_merge_rules_pin_the_measured_choices():
     """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
