@@ -1886,10 +1886,16 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 // output fp32).  Same row-parallel rotation loop as qbuild_kernel; a skipped
 // pair contributes the identity (phase 1 writes it: T1 is read by update and
 // phase 2 even when its pair did not rotate).
-template <int PHASE, int R, int NT>
+// NP > 0 (phase 2 with R = 8): instead of the fp32 T, T - I is written
+// straight in the apply's split-bf16 fragment layout (what tsplit_kernel
+// makes from T): a thread's 8 rows k0 .. k0 + 7 of one column are exactly one
+// A-operand fragment (k block k0 / 16, lane half (k0 / 8) & 1).
+template <int PHASE, int R, int NT, int NP = 0>
 __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
     const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
-    const int32_t* __restrict__ skip, double* __restrict__ T1, float* __restrict__ Tq) {
+    const int32_t* __restrict__ skip, double* __restrict__ T1, float* __restrict__ Tq,
+    bf16x8* __restrict__ Ts = nullptr) {
+  static_assert(NP == 0 || (PHASE == 2 && R == 8), "direct split T: phase 2, 8 rows per thread");
   constexpr int W = 64, N = 2 * W, QN = 4 * W;
   constexpr int WAVES = NT / SVDJ_WAVE;
   static_assert((PHASE == 1 ? N : QN) % (R * WAVES) == 0, "row cover");
@@ -1949,13 +1955,33 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
       qo[(size_t)(k0 + i) * N + a] = qx[i];
       qo[(size_t)(k0 + i) * N + W + yr] = qy[i];
     }
-  } else {
+  } else if constexpr (NP == 0) {
     float* qo = Tq + (size_t)q * QN * QN;
     const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       qo[(size_t)(k0 + i) * QN + xc] = (float)qx[i];
       qo[(size_t)(k0 + i) * QN + yc] = (float)qy[i];
+    }
+  } else {  // Ts[q][kb][ct][part][lane (c, h)] element e = (T - I)[16 kb + 8h + e][32 ct + c]
+    const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
+    const int kb = k0 >> 4, hh = (k0 >> 3) & 1;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int col = side ? yc : xc;
+      bf16x8 parts[NP];
+#pragma unroll
+      for (int e = 0; e < R; ++e) {
+        __bf16 pp[NP];
+        // T rounded to fp32 first (the T the tsplit path splits), then T - I
+        const float t = (float)(side ? qy[e] : qx[e]) - (k0 + e == col ? 1.0f : 0.0f);
+        split_bf16<NP>(t, pp);
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) parts[pi][e] = pp[pi];
+      }
+      bf16x8* dst = Ts + ((((size_t)q * 16 + kb) * 8 + (col >> 5)) * NP) * SVDJ_WAVE + (col & 31) + 32 * hh;
+#pragma unroll
+      for (int pi = 0; pi < NP; ++pi) dst[pi * SVDJ_WAVE] = parts[pi];
     }
   }
 }
@@ -1972,7 +1998,10 @@ constexpr int kUpdThreads = 256;
 __global__ __launch_bounds__(kUpdThreads) void quad_update_kernel(
     const float* __restrict__ slabs, int gch, const double* __restrict__ T1,
     float* __restrict__ upd) {
-  constexpr int W = 64, N = 2 * W, MP = N + 4, HP = 32 + 4;
+  // M's row stride is odd (129 = 1 mod 64 banks): its transposed fill and
+  // both read orders are conflict-free (MP = N + 4 had 52 % bank-conflict
+  // cycles, profiles/r5_prof_final)
+  constexpr int W = 64, N = 2 * W, MP = N + 1, HP = 32 + 4;
   using M = Mfma<float>;
   __shared__ float Ms[N * MP];
   __shared__ float Rs[N * HP];  // R[:, 32 oj .. + 32]
@@ -2387,6 +2416,10 @@ struct GramQLds {
   static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
 };
 static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
+// ABL (tools/micro/quad_apply_ab.hip only; production launches ABL = 0):
+// bit 0 one MFMA per output tile and k step instead of 6; bit 1 no global
+// reads (no DMA, no waits).
+template <int ABL = 0>
 __global__ __launch_bounds__(kGramQThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
                  int P, int rows_per_chunk, float* __restrict__ slabs) {
@@ -2410,6 +2443,7 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   // lane, lanes at a 128-byte column stride) then spread over all banks
   // instead of piling onto a few (35 % bank-conflict cycles unswizzled)
   auto dma = [&](int sl, int buf) {
+    if constexpr ((ABL & 2) != 0) return;
     const int r0 = r_begin + 32 * sl;
     char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
     const int jr = ((lane & 7) ^ (lane >> 3)) * 4;  // col & 7 == lane >> 3 for every i
@@ -2423,7 +2457,8 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   for (int j = 0; j < 3; ++j) acc[j] = lo[j] = Mfma<float>::zero();
   auto slab = [&](int sl, auto bufc) {
     constexpr int buf = decltype(bufc)::value;
-    if (sl + 1 < ns) wait_vmcnt<4>();
+    if constexpr ((ABL & 2) != 0) {
+    } else if (sl + 1 < ns) wait_vmcnt<4>();
     else wait_vmcnt<0>();
     {  // split column tile `wave` of this slab: rows 16 kk + 8h .. + 7 of column c
       const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
@@ -2460,8 +2495,18 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
           xf[i] = Sr[((kk * 8 + cx) * NP + i) * SVDJ_WAVE];
           yf[i] = Sr[((kk * 8 + cy) * NP + i) * SVDJ_WAVE];
         }
-        lo[j] = mfma_split<NP, 1>(xf, yf, lo[j]);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf[0], yf[0], acc[j], 0, 0, 0);
+        if constexpr ((ABL & 1) != 0) {
+          using i32x4 = __attribute__((ext_vector_type(4))) int;
+          i32x4 xx = __builtin_bit_cast(i32x4, xf[0]) ^ __builtin_bit_cast(i32x4, xf[1]) ^
+                     __builtin_bit_cast(i32x4, xf[2]);
+          i32x4 yy = __builtin_bit_cast(i32x4, yf[0]) ^ __builtin_bit_cast(i32x4, yf[1]) ^
+                     __builtin_bit_cast(i32x4, yf[2]);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xx),
+                                                         __builtin_bit_cast(bf16x8, yy), acc[j], 0, 0, 0);
+        } else {
+          lo[j] = mfma_split<NP, 1>(xf, yf, lo[j]);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf[0], yf[0], acc[j], 0, 0, 0);
+        }
       }
     if (sl + 2 < ns) dma(sl + 2, buf);
   };
@@ -2717,7 +2762,7 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     const int b = s & 1;
     const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
     const int32_t* pr1 = pr + 2 * c.P;
-    hipLaunchKernelGGL(gram_quad_kernel, dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0, c.st,
+    hipLaunchKernelGGL(gram_quad_kernel<0>, dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0, c.st,
                        c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
     SVDJ_LAUNCH_CHECK();
     // many row chunks (few quads): sum them once, wide, for both consumers
@@ -2759,18 +2804,23 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     if (lat)
       hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, QBT>), dim3(c.P, 256 / (2 * QBW)), dim3(QBT), 0,
                          c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+    else if (mma == 2)  // 8 rows per thread: the split T is written directly (no tsplit pass)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT, 2>), dim3(c.P, 256 / (R * QBW)), dim3(QBT),
+                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq, c.Ts[b]);
     else
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT>), dim3(c.P, 256 / (R * QBW)), dim3(QBT), 0,
-                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT, 3>), dim3(c.P, 256 / (R * QBW)), dim3(QBT),
+                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq, c.Ts[b]);
     SVDJ_LAUNCH_CHECK();
-    const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
-    if (mma == 2)
-      hipLaunchKernelGGL((tsplit_kernel<2>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
-                         c.skip1[b], c.skip2[b]);
-    else
-      hipLaunchKernelGGL((tsplit_kernel<3>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
-                         c.skip1[b], c.skip2[b]);
-    SVDJ_LAUNCH_CHECK();
+    if (lat) {  // 2 rows per thread: fp32 T, then the split pass
+      const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
+      if (mma == 2)
+        hipLaunchKernelGGL((tsplit_kernel<2>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
+                           c.skip1[b], c.skip2[b]);
+      else
+        hipLaunchKernelGGL((tsplit_kernel<3>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
+                           c.skip1[b], c.skip2[b]);
+      SVDJ_LAUNCH_CHECK();
+    }
     return 0;
   } else {
     (void)c; (void)s; (void)tol; (void)absmode; (void)max_inner; (void)metric; (void)mma;
@@ -3115,7 +3165,7 @@ extern "C" int svdj_gram_quad(const void* A, int lda, int m_pad, const int32_t* 
     return -2;
   }
   const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
-  hipLaunchKernelGGL(gram_quad_kernel, dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
+  hipLaunchKernelGGL(gram_quad_kernel<0>, dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
                      (hipStream_t)stream, (const float*)A, lda, m_pad, pairs, P, rows_per_chunk,
                      (float*)slabs);
   const hipError_t e = hipGetLastError();

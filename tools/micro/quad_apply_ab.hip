@@ -7,6 +7,8 @@
 //   2 no global memory; 3 = 1 + 2; 4 no MFMA loop (DMA, split, epilogue);
 //   6 = 4 + 2 (split and epilogue only); 8 never the cheap k-half form; the
 //   production form on small T - I (every k half cheap); and the NP = 2 (3-MFMA) form.
+// Then the quad Gram (gram_quad_kernel) on the same A: production, one MFMA
+// per tile and k step, no global reads, both.
 // Prints one JSON line per variant: best and median of 12 timed launches.
 // Build (post.o: the library's helpers it links against):
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I svd-jacobi-mpi-cuda_amd/csrc/include
@@ -78,6 +80,34 @@ static int run(const char* name, float* A, float* V, int m, int nq, const int32_
   return 0;
 }
 
+template <int ABL>
+static int run_gram(const char* name, const float* A, int m, int nq, const int32_t* pairs,
+                    float* slabs, int gch) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> t;
+  const int rows = m / gch;
+  for (int it = 0; it < 14; ++it) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(gram_quad_kernel<ABL>, dim3(nq, gch), dim3(kGramQThreads), 0, 0, A, m, m, pairs,
+                       2 * nq, rows, slabs);
+    CK(hipGetLastError());
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (it >= 2) t.push_back(ms * 1e3f);
+  }
+  std::sort(t.begin(), t.end());
+  const double bytes = (double)nq * 256 * m * 4;
+  printf("{\"kernel\": \"gram_quad\", \"variant\": \"%s\", \"abl\": %d, \"chunks\": %d, "
+         "\"best_us\": %.1f, \"median_us\": %.1f, \"read_TB_s_at_best\": %.3f}\n",
+         name, ABL, gch, t[0], t[t.size() / 2], bytes / (t[0] * 1e-6) / 1e12);
+  fflush(stdout);
+  return 0;
+}
+
 int main() {
   const int m = 16384, nblk = 256, nq = nblk / 4;
   const size_t nA = (size_t)nblk * 64 * m;
@@ -123,5 +153,12 @@ int main() {
   CK(hipDeviceSynchronize());
   if (run<2, 0>("production_np2", A, V, m, nq, pairs, Ts, skip, bytes)) return 1;
   if (run<2, 2>("np2_no_global_memory", A, V, m, nq, pairs, Ts, skip, bytes)) return 1;
+  // the quad Gram at the same geometry (4 row chunks per quad, as the merged step)
+  float* slabs;
+  CK(hipMalloc(&slabs, (size_t)3 * 2 * nq * 4 * 64 * 64 * 4));
+  if (run_gram<0>("production", A, m, nq, pairs, slabs, 4)) return 1;
+  if (run_gram<1>("one_mfma", A, m, nq, pairs, slabs, 4)) return 1;
+  if (run_gram<2>("no_global_memory", A, m, nq, pairs, slabs, 4)) return 1;
+  if (run_gram<3>("one_mfma_no_memory", A, m, nq, pairs, slabs, 4)) return 1;
   return 0;
 }
