@@ -523,6 +523,32 @@ def run_native(a, dtype, work):
         dist.destroy_process_group()
 
 
+def work_estimate(counts, m_pad, seconds):
+    """Executed matrix-core work and HBM traffic of the quad kernels per
+    solve, next to the algorithmic GFLOP/s (the headline is the
+    reference's scalar-Jacobi flop count, which is not what the MFMAs
+    execute).  counts = [apply MFMAs, apply tiles, quad Grams] summed over
+    ranks: one v_mfma_f32_32x32x16_bf16 = 32768 flops; an apply tile is 32
+    rows x 256 columns of A or V read and written (64 KiB); a quad Gram reads
+    256 columns of m_pad rows and issues 288 MFMAs per 32-row slab.  Averaged
+    over the whole time to converge, so these are lower bounds on the quad
+    kernels' own rates (the EVD chain and the single steps that open each
+    sweep are in the time but not in the counts)."""
+    mf_apply, tiles, gq = counts
+    mf_gram = gq * (m_pad / 32.0) * 288.0
+    flops = (mf_apply + mf_gram) * 32768.0
+    nbytes = tiles * 65536.0 + gq * m_pad * 256.0 * 4.0
+    if seconds <= 0 or flops <= 0:
+        return None
+    return {"basis": "quad-step kernels only (split-bf16 apply + quad Gram), device-counted; "
+                     "per solve, averaged over the time to converge",
+            "mfma_bf16_tflop_per_solve": round(flops / 1e12, 3),
+            "executed_mfma_tflops": round(flops / seconds / 1e12, 1),
+            "hbm_gb_per_solve": round(nbytes / 1e9, 1),
+            "hbm_tb_per_s": round(nbytes / seconds / 1e12, 3),
+            "apply_mfma": int(mf_apply), "apply_tiles": int(tiles), "quad_grams": int(gq)}
+
+
 def want_sigma(a, n) -> bool:
     """sigma vs the fp64 oracle: by default whenever n <= 8192 (rocSOLVER
     svdvals of the regenerated A in fp64, after timing); --check-sigma forces
@@ -692,6 +718,13 @@ def main():
             err = sigma_check(last, gen, m, n, comm)
         if comm.rank == 0:
             acc = dict(acc or {}, sigma_max_rel_err_vs_fp64_oracle=err)
+    # work the quad kernels actually did in the last solve, summed over ranks
+    # (apply MFMAs and tiles counted on the device, quad Grams on the host)
+    wk = last.info.get("work") or {}
+    wt = torch.tensor([float(wk.get("apply_mfma", 0)), float(wk.get("apply_tiles", 0)),
+                       float(wk.get("gram_quads", 0))], dtype=torch.float64, device=comm.device)
+    comm.allreduce_sum_(wt)
+    work_est = work_estimate(wt.cpu().tolist(), int(wk.get("m_pad", m)), ms / 1e3)
     if comm.rank == 0:
         line = {
             "metric": BASELINE_METRIC,
@@ -735,6 +768,7 @@ def main():
             "world": ready.get("world"), "devices": ready.get("devices"),
             "rccl_ranks": ready.get("rccl_ranks"), "p2p_partners": ready.get("p2p_partners"),
             "accuracy": acc,
+            "work_estimate": work_est,
         }
         print(json.dumps(line), flush=True)
         if a.json_out:

@@ -2147,6 +2147,7 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
@@ -2161,7 +2162,7 @@ __global__ __launch_bounds__(kQuadTsThreads) __attribute__((amdgpu_waves_per_eu(
 apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
                      int v_tiles, const int32_t* __restrict__ pairs, int nq,
                      const bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
-                     const int32_t* __restrict__ skip2) {
+                     const int32_t* __restrict__ skip2, uint32_t* __restrict__ work = nullptr) {
   using L = QuadTsLds<NP>;
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int lane = threadIdx.x & 63;
@@ -2322,7 +2323,10 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       acc += lo;
       // 4. own raw values, still in this wave's raw image R[buf] (its refill,
       //    tile t + 2, is issued below), and the delta-form store, in place
-      //    (acc layout: register 4g + i is own column 8g + 4h + i, row c)
+      //    (acc layout: register 4g + i is own column 8g + 4h + i, row c).
+      //    (Staging the finished tile through R[buf] for 16-byte stores cut
+      //    the compute-only time 1229 -> 1037 us but not the solve's:
+      //    profiles/r6_apply/ablation_vector_epilogue_rejected.jsonl.)
       {
         const bool isA = t < a_tiles;
         float* const own = isA ? ownA : ownV;
@@ -2360,6 +2364,13 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       if (cheap == 1) run(std::integral_constant<int, 1>{});
       else if (cheap == 2) run(std::integral_constant<int, 2>{});
       else run(std::integral_constant<int, 3>{});
+    }
+    // work counters of the sweep (metric words 6, 7; svdj_stop.h): MFMAs this
+    // wave issued in units of 24 (96, 72 or 48 per tile), and tiles moved
+    if (work && lane == 0) {
+      const uint32_t per = NP == 3 ? 4u - (cheap & 1u) - ((cheap >> 1) & 1u) : 2u;
+      atomicAdd(&work[0], (uint32_t)(t1 - t0) * per);
+      if (wave == 0) atomicAdd(&work[1], (uint32_t)(t1 - t0));
     }
     // the next item re-stages both images
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2903,7 +2914,7 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
 }
 
 template <typename T, int W>
-static int launch_apply(const Chain<T>& c, int s, int mma) {
+static int launch_apply(const Chain<T>& c, int s, int mma, uint32_t* metric) {
   const int b = s & 1;
   const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
   const int nv = c.V ? c.n_v : 0, ych = c.V ? c.g.v_chunks : 0;
@@ -2917,14 +2928,15 @@ static int launch_apply(const Chain<T>& c, int s, int mma) {
       }
       // T-stationary persistent apply (apply_quad_ts_kernel)
       const int nq = c.P / 2, at = c.m_pad / 32, vt = c.V ? c.n_v / 32 : 0;
+      uint32_t* work = metric ? metric + 6 : nullptr;
       if (mma == 1)
         hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b]);
+                           c.skip2[b], work);
       else
         hipLaunchKernelGGL((apply_quad_ts_kernel<2>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b]);
+                           c.skip2[b], work);
       SVDJ_LAUNCH_CHECK();
       return 0;
     } else {
@@ -2972,7 +2984,7 @@ static int block_steps_t(const Chain<T>& c, double tol, int absmode, int max_inn
                          uint32_t* metric, int mma) {
   for (int s = 0; s < c.steps; ++s) {
     int rc = launch_gram_evd<T, W>(c, s, tol, absmode, max_inner, metric, mma);
-    if (!rc) rc = launch_apply<T, W>(c, s, mma);
+    if (!rc) rc = launch_apply<T, W>(c, s, mma, metric);
     if (rc) return rc;
   }
   return 0;

@@ -24,7 +24,10 @@
 //       sine, with the factor n instead of the rotation count).
 // The metric words a sweep accumulates on the device (uint32 each):
 //   [0] mx (float bits), [1] rotated block pairs, [2..3] the negligible-column
-//   floor (double, set once per solve), [4] ms (float bits), [5] R, [6..7] spare.
+//   floor (double, set once per solve), [4] ms (float bits), [5] R, and two
+//   work counters of the quad apply (not part of the stop test): [6] MFMAs
+//   issued / 24 (one 32x32x16 bf16 MFMA = 32768 flops), [7] 32-row tiles of
+//   256 columns moved (read and written once each).
 #pragma once
 
 #define SVDJ_METRIC_WORDS 8

@@ -149,6 +149,17 @@ def metric_stop_values(metric: torch.Tensor) -> torch.Tensor:
     return torch.stack([f[0].double(), f[4].double(), metric[1].double(), u])
 
 
+def metric_work(metric: torch.Tensor) -> torch.Tensor:
+    """The quad apply's work counters of the sweep (svdj_stop.h words 6, 7),
+    float64 on the metric's device without a host sync: [MFMAs issued / 24,
+    32-row x 256-column tiles moved].  Zeros for CPU metrics (the CPU
+    emulation has no counters)."""
+    if metric.device.type == "cpu":
+        return torch.zeros(2, dtype=torch.float64)
+    w = metric[6:8].double()
+    return torch.where(w < 0, w + 2.0 ** 32, w)
+
+
 def read_stop(metric: torch.Tensor):
     """(max convergence value, max effective sine, rotated pairs, column
     rotations) -- synchronises."""
@@ -440,7 +451,7 @@ def block_solve(At, Vt, D, m_pad, W, tol, max_inner, max_sweeps, mma="native",
 
 __all__ = [
     "NativeError", "ROW_ALIGN", "SUPPORTED_BLOCK", "INNER_ORDERS", "step_modes", "dtype_code", "new_metric", "reset_metric", "set_norm_floor",
-    "METRIC_WORDS", "read_stop", "metric_stop_values", "sweep_converged", "STOP_RULES",
+    "METRIC_WORDS", "read_stop", "metric_stop_values", "metric_work", "sweep_converged", "STOP_RULES",
     "read_metric", "set_identity", "col_norms2", "finalize", "scalar_step", "scalar_solve",
     "block_workspace", "block_steps", "block_solve", "check_block", "MMA_CODES", "mma_code",
     "apply_q",

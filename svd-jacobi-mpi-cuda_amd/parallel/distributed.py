@@ -315,11 +315,18 @@ class DistributedBlockJacobi(Solver):
         t0 = time.perf_counter()
         converged = False
         bufs = (rA, rV, rD)
+        # work actually done by the quad kernels (bench.py's executed-MFMA and
+        # HBM estimates): device counters of the apply, summed per sweep without
+        # a host sync, and the quad Grams issued
+        work = {"gram_quads": 0}
+        work_acc = torch.zeros(2, dtype=torch.float64, device=metric.device)
         if pipelined:
             ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
                                   parts=splan.parts, exchange=cfg.exchange)
 
             def run_steps(pairs, modes, slot):
+                # quads of the quad steps issued (each runs the quad Gram): host count
+                work["gram_quads"] += sum(1 for x in modes if int(x) == 4) * (pairs.shape[1] // 2)
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                               inner_order=inner)
@@ -354,6 +361,7 @@ class DistributedBlockJacobi(Solver):
                                       cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
                                       tol_mode=cfg.tol_mode, inner_order=inner)
                 mx, ms, nrot, ncr = self._reduce_metric(metric, dev)
+                work_acc += K.metric_work(metric)
             hist.append(mx)
             sweeps = sw + 1
             if cfg.progress and g == 0:
@@ -385,7 +393,10 @@ class DistributedBlockJacobi(Solver):
         sigma_loc = K.finalize(At, m_pad, scale_u=jobu != SVDOptions.NoVec)
         sync()
         t_total = time.perf_counter() - t0
-        info = {"tol": tol, "converged": converged, "stop_reason": stop_reason,
+        wa = work_acc.cpu()
+        info_work = {"apply_mfma": int(wa[0]) * 24, "apply_tiles": int(wa[1]),
+                     "gram_quads": int(work["gram_quads"]), "m_pad": m_pad}
+        info = {"tol": tol, "converged": converged, "stop_reason": stop_reason, "work": info_work,
                 "stop_rule": cfg.stop_rule, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "inner_order": inner, "quad": quad, "merged_chains": bool(pipelined and merged),
                 "exchange": ex.exchange if pipelined else "direct",
