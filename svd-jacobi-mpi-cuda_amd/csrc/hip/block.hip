@@ -1886,10 +1886,17 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 // output fp32).  Same row-parallel rotation loop as qbuild_kernel; a skipped
 // pair contributes the identity (phase 1 writes it: T1 is read by update and
 // phase 2 even when its pair did not rotate).
+// First element of the split T - I fragment (quad q, 32-row k block kb, 32-column
+// tile ct, 16-column sub-tile cs) in the apply's A-operand layout
+// (tsplit_kernel, apply_quad_ts_kernel): NP parts of SVDJ_WAVE bf16x8 each.
+__host__ __device__ constexpr size_t ts_frag(int q, int kb, int ct, int cs, int np) {
+  return ((((size_t)q * 8 + kb) * 8 + ct) * 2 + cs) * np * SVDJ_WAVE;
+}
+
 // NP > 0 (phase 2 with R = 8): instead of the fp32 T, T - I is written
 // straight in the apply's split-bf16 fragment layout (what tsplit_kernel
 // makes from T): a thread's 8 rows k0 .. k0 + 7 of one column are exactly one
-// A-operand fragment (k block k0 / 16, lane half (k0 / 8) & 1).
+// A-operand fragment (k block k0 / 32, lane group (k0 / 8) & 3).
 template <int PHASE, int R, int NT, int NP = 0>
 __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
     const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
@@ -1963,9 +1970,10 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
       qo[(size_t)(k0 + i) * QN + xc] = (float)qx[i];
       qo[(size_t)(k0 + i) * QN + yc] = (float)qy[i];
     }
-  } else {  // Ts[q][kb][ct][part][lane (c, h)] element e = (T - I)[16 kb + 8h + e][32 ct + c]
+  } else {  // tsplit_kernel's layout: element e of lane 16g + i of fragment (kb, ct, cs)
+            // = (T - I)[32 kb + 8g + e][32 ct + 16 cs + i]
     const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
-    const int kb = k0 >> 4, hh = (k0 >> 3) & 1;
+    const int kb = k0 >> 5, gg = (k0 >> 3) & 3;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const int col = side ? yc : xc;
@@ -1979,7 +1987,7 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) parts[pi][e] = pp[pi];
       }
-      bf16x8* dst = Ts + ((((size_t)q * 16 + kb) * 8 + (col >> 5)) * NP) * SVDJ_WAVE + (col & 31) + 32 * hh;
+      bf16x8* dst = Ts + ts_frag(q, kb, col >> 5, (col >> 4) & 1, NP) + (col & 15) + 16 * gg;
 #pragma unroll
       for (int pi = 0; pi < NP; ++pi) dst[pi * SVDJ_WAVE] = parts[pi];
     }
@@ -2083,9 +2091,10 @@ __global__ __launch_bounds__(kUpdThreads) void quad_update_kernel(
 }
 
 // T - I of every quad split into NP bf16 parts (split_bf16), in the A-operand
-// order of v_mfma_f32_32x32x16_bf16: entry [q][kb][ct][part][lane (c, h)]
-// element e = (T - I)[kb 16 + 8h + e][ct 32 + c].  One thread per
-// fragment; skipped quads are left alone (the apply skips them too).
+// order of v_mfma_f32_16x16x32_bf16: entry [q][kb][ct][cs][part][lane (i, g)]
+// element e = (T - I)[32 kb + 8g + e][32 ct + 16 cs + i], lane = 16g + i.
+// One thread per fragment; skipped quads are left alone (the apply skips them
+// too).  (qbuild_quad_kernel<2, 8, ., NP> writes the same layout directly.)
 constexpr int kTsplitThreads = 256;
 template <int NP>
 __global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
@@ -2094,9 +2103,9 @@ __global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
   constexpr int QN = 256;
   const int q = blockIdx.x;
   if (skip1[2 * q] && skip1[2 * q + 1] && skip2[2 * q] && skip2[2 * q + 1]) return;
-  const int idx = blockIdx.y * kTsplitThreads + threadIdx.x;  // < 16 * 8 * 64
-  const int kb = idx >> 9, ct = (idx >> 6) & 7, lane = idx & 63;
-  const int col = ct * 32 + (lane & 31), k0 = kb * 16 + 8 * (lane >> 5);
+  const int idx = blockIdx.y * kTsplitThreads + threadIdx.x;  // < 8 * 8 * 2 * 64
+  const int kb = idx >> 10, ct = (idx >> 7) & 7, cs = (idx >> 6) & 1, lane = idx & 63;
+  const int col = ct * 32 + cs * 16 + (lane & 15), k0 = kb * 32 + 8 * (lane >> 4);
   const float* src = Tq + (size_t)q * QN * QN + col;
   bf16x8 parts[NP];
 #pragma unroll
@@ -2107,28 +2116,39 @@ __global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
 #pragma unroll
     for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
   }
-  bf16x8* dst = Ts + ((((size_t)q * 16 + kb) * 8 + ct) * NP) * SVDJ_WAVE + lane;
+  bf16x8* dst = Ts + ts_frag(q, kb, ct, cs, NP) + lane;
 #pragma unroll
   for (int i = 0; i < NP; ++i) dst[i * SVDJ_WAVE] = parts[i];
 }
 
-// [a b c d] <- [a b c d] T, T-STATIONARY (round 5).  The round-4 apply
-// streamed the 384 KB split T through LDS for every 128-row tile (3.2 GB of T
-// per 64-pair quad step against 2.1 GB of data; 1.71 ms per 128-pair quad
-// step, profiles/r4_quad).  Here a workgroup keeps T in REGISTERS for
-// thousands of rows:
+// [a b c d] <- [a b c d] T, T-STATIONARY (round 5; 16x16x32 MFMAs round 6).
+// The round-4 apply streamed the 384 KB split T through LDS for every 128-row
+// tile (3.2 GB of T per 64-pair quad step against 2.1 GB of data; 1.71 ms per
+// 128-pair quad step, profiles/r4_quad).  Here a workgroup keeps T in
+// REGISTERS for thousands of rows:
 //   * 8 waves (two per SIMD), wave w owns output column tile w (32 of the
-//     quad's 256 columns) and holds its split T - I slice, 16 k blocks x NP
-//     bf16x8 = 192 VGPRs for NP = 3, for the whole launch;
+//     quad's 256 columns, two 16-column sub-tiles) and holds its split T - I
+//     slice, 8 k blocks of 32 x 2 sub-tiles x NP bf16x8 = 192 VGPRs for
+//     NP = 3, for the whole launch;
 //   * the workgroup walks a contiguous range of 32-row tiles of A then V
 //     (every tile all 256 columns: it owns its rows, so in place is safe);
 //   * each wave LDS-DMAs (global_load_lds_dwordx4) its own 32 columns of the
 //     tile two tiles ahead into a wave-private raw image (no VGPRs in
-//     flight), splits them into the shared B-fragment image of the tile
-//     (double-buffered, one barrier per tile), runs 16 k blocks x (1 + 5)
-//     MFMAs (leading product and the small ones in two accumulators, as
-//     apply_split_kernel), and reads its own raw values for the delta-form
-//     epilogue Y = X + X (T - I) back from its raw image.
+//     flight), splits them -- exactly k block w -- into the shared B-fragment
+//     image of the tile (double-buffered, one barrier per tile), runs 8 k
+//     blocks x 2 x 2 sub-tiles x (1 + 5) v_mfma_f32_16x16x32_bf16 (leading
+//     product and the small ones in two accumulators, as apply_split_kernel),
+//     and reads its own raw values for the delta-form epilogue
+//     Y = X + X (T - I) back from its raw image.
+// MFMA shape (round 6): the kernel is power-limited -- the dense form runs at
+// 1.77 GHz with its matrix pipe 61 % busy at that clock, without global
+// memory at 2.10 GHz, memory alone at 2.45 GHz (profiles/r6_clock) -- and the
+// 16x16x32 bf16 MFMA holds a higher clock than 32x32x16 for the same flops
+// (MI355X_MICROARCH "DVFS give-back" (7)); same cycles, registers and LDS
+// reads per flop.
+// (The raw image is plain [col][row]: the split's and epilogue's dword reads
+// meet 2-way bank conflicts, which cost less than the registers a swizzle's
+// extra lane offsets took from the T slice.)
 // Work: the active quads (some step-s or step-(s+1) pair rotated) are listed
 // by every wave with ballots over the skip flags (no extra launch, no host
 // sync); nact active quads x S row slices, S = max(1, grid / nact), are dealt
@@ -2147,14 +2167,17 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
 
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // ABL (tools/micro/quad_apply_ab.hip only; production launches ABL = 0):
-// bit 0 one MFMA per k block instead of 1 + (products of order < NP), B
-// fragments still read; bit 1 no global memory (no DMA, no waits, no
+// bit 0 one MFMA per k block and sub-tile instead of 1 + (products of order
+// < NP), B fragments still read; bit 1 no global memory (no DMA, no waits, no
 // stores); bit 2 no MFMA loop at all (split, barrier, epilogue, DMA only);
 // bit 3 never the cheap (first-order) k-block form.
 template <int NP, int ABL = 0>
@@ -2167,7 +2190,7 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = lane & 31, h = lane >> 5;
+  const int i16 = lane & 15, g = lane >> 4;
   auto active = [&](int q) -> bool {  // all four flags loaded (no short-circuit branches)
     if (q >= nq) return false;
     return (skip1[2 * q] & skip1[2 * q + 1] & skip2[2 * q] & skip2[2 * q + 1]) == 0;
@@ -2194,33 +2217,37 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
     }
     q = __builtin_amdgcn_readfirstlane(q);
     const int t0 = (int)((long long)sl * nt / S), t1 = (int)((long long)(sl + 1) * nt / S);
-    // this wave's split T - I slice: Ts[q][kb][ct = wave][part][lane]
-    bf16x8 qf[16][NP];
-    {
-      const bf16x8* tp = Ts + ((size_t)q * 16 * 8 + wave) * NP * SVDJ_WAVE + lane;
+    // this wave's split T - I slice: Ts[q][kb][ct = wave][cs][part][lane]
+    bf16x8 qf[8][2][NP];
 #pragma unroll
-      for (int kb = 0; kb < 16; ++kb)
+    for (int kb = 0; kb < 8; ++kb)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) qf[kb][p] = tp[(kb * 8 * NP + p) * SVDJ_WAVE];
-    }
-    // Halves of the k range (k blocks 0-7 = blocks a, b of the quad, 8-15 =
+      for (int cs = 0; cs < 2; ++cs) {
+        const bf16x8* tp = Ts + ts_frag(q, kb, wave, cs, NP) + lane;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) qf[kb][cs][p] = tp[p * SVDJ_WAVE];
+      }
+    // Halves of the k range (k blocks 0-3 = blocks a, b of the quad, 4-7 =
     // c, d) whose slice of T - I is below 2^-9 in magnitude: there the
     // order-2 products (q0 x2, q1 x1, q2 x0 <= 3 2^-18 |t||x| <= 3 2^-27 |x|,
     // below the fp32 rounding of the output) are dropped, 3 MFMAs per k block
-    // instead of 6.  With T = T1 T2 (pairs (a,c), (b,d) then (a,d), (b,c)),
-    // for an output column in a or b the rows of a and b are second order in
-    // the rotation angles (T_aa - I, T_ba = T1_bd T2_da), those of c and d
-    // first order; for c or d the other way round -- so once the angles are
-    // below ~0.04 one half of every column tile takes the cheap form.
+    // and sub-tile instead of 6.  With T = T1 T2 (pairs (a,c), (b,d) then
+    // (a,d), (b,c)), for an output column in a or b the rows of a and b are
+    // second order in the rotation angles (T_aa - I, T_ba = T1_bd T2_da),
+    // those of c and d first order; for c or d the other way round -- so once
+    // the angles are below ~0.04 one half of every column tile takes the
+    // cheap form.
     uint32_t cheap = 0;
     if constexpr (NP == 3 && (ABL & 8) == 0) {
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         float mx = 0.0f;
 #pragma unroll
-        for (int kb = 8 * hf; kb < 8 * hf + 8; ++kb)
+        for (int kb = 4 * hf; kb < 4 * hf + 4; ++kb)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf((float)qf[kb][0][e]));
+          for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf((float)qf[kb][cs][0][e]));
         if (wave_max(mx) <= 0.001953125f) cheap |= 1u << hf;
       }
       cheap = __builtin_amdgcn_readfirstlane(cheap);
@@ -2232,20 +2259,27 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
     float* const ownA = A + (size_t)col0 * lda;
     float* const ownV = V ? V + (size_t)col0 * ldv : nullptr;
 
-    auto dma = [&](int t, int buf) {  // raw tile t, own 32 columns -> R[buf] (4 x 1 KB)
+    // raw tile t, own 32 columns -> R[buf] (4 x 1 KB): lane -> column
+    // 8i + lane / 8, row chunk lane % 8 (one 32-bit lane offset from a
+    // wave-uniform column base)
+    auto dma = [&](int t, int buf) {
       if constexpr ((ABL & 2) != 0) return;
       const bool isA = t < a_tiles;
       const float* base = isA ? ownA : ownV;
       const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
       char* dst = lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096;
+      const uint32_t o = (uint32_t)((lane >> 3) * ld + (lane & 7) * 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds(base + (size_t)(8 * i + (lane >> 3)) * ld + r0 + (lane & 7) * 4,
-                                         dst + i * 1024, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(&at_u32(base + (size_t)(8 * i) * ld + r0, o), dst + i * 1024,
+                                         16, 0, 0);
     };
+    // lane bases into the raw image [col][row]: split reads (column 8g + e,
+    // row 16 rs + i) and epilogue reads (column 16 cs + 4g + e, row 16 rs + i)
+    const int sb = 256 * g + i16, eb = 128 * g + i16;
     auto tile = [&](int t, auto bufc, auto chc) {
       constexpr int buf = decltype(bufc)::value;
-      constexpr int CH = decltype(chc)::value;  // cheap halves (bit 0: k blocks 0-7, bit 1: 8-15)
+      constexpr int CH = decltype(chc)::value;  // cheap halves (bit 0: k blocks 0-3, bit 1: 4-7)
       // 1. own DMA of tile t landed (younger: stores of t-1, DMA of t+1)
       const int younger = (t > t0 ? 16 : 0) + (t + 1 < t1 ? 4 : 0);
       if constexpr ((ABL & 2) != 0) (void)younger;
@@ -2253,96 +2287,103 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       else if (younger == 16) wait_vmcnt<16>();
       else if (younger == 4) wait_vmcnt<4>();
       else wait_vmcnt<0>();
-      // 2. split own columns into the shared B-fragment image S[buf]
+      const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
+      // 2. split own columns (k block `wave`) into the shared B-fragment image
+      //    S[buf]: [kb][rs][part][lane (i, g)] element e = X[16 rs + i][32 kb + 8g + e]
       {
-        const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
         bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
-        for (int kbl = 0; kbl < 2; ++kbl) {
+        for (int rs = 0; rs < 2; ++rs) {
           bf16x8 parts[NP];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             __bf16 pp[NP];
-            split_bf16<NP>(R[(16 * kbl + 8 * h + e) * 32 + c], pp);
+            split_bf16<NP>(R[sb + 32 * e + 16 * rs], pp);
 #pragma unroll
             for (int i = 0; i < NP; ++i) parts[i][e] = pp[i];
           }
 #pragma unroll
-          for (int i = 0; i < NP; ++i) Sw[((2 * wave + kbl) * NP + i) * SVDJ_WAVE] = parts[i];
+          for (int i = 0; i < NP; ++i) Sw[((2 * wave + rs) * NP + i) * SVDJ_WAVE] = parts[i];
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // 3. 16 k blocks x (1 + 5) MFMAs (1 + 2 in a cheap half) against the
-      //    register-resident slice
+      // 3. per 16-row half rs of the tile: 8 k blocks x 2 column sub-tiles x
+      //    (1 + 5) MFMAs (1 + 2 in a cheap half) against the register-resident
+      //    slice, then that half's epilogue (one half's accumulators live at a
+      //    time: 16 VGPRs, what lets the T slice stay in registers)
       const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
-      f32x16 acc = Mfma<float>::zero(), lo = Mfma<float>::zero();
-      // k blocks [k0, k0 + 8): first-order products only (cheap half) or all
-      // products of order < NP
-      auto khalf = [&](auto k0c) {
-        constexpr int k0 = decltype(k0c)::value;
-        if constexpr (NP == 3 && ((CH >> (k0 / 8)) & 1) != 0) {
+      const bool isA = t < a_tiles;
+      float* const own = isA ? ownA : ownV;
+      const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
+      const uint32_t st_off = (uint32_t)(4 * g * ld + i16) + (uint32_t)r0;
 #pragma unroll
-          for (int kb = k0; kb < k0 + 8; ++kb) {
-            const bf16x8 x0 = Sr[(kb * NP + 0) * SVDJ_WAVE], x1 = Sr[(kb * NP + 1) * SVDJ_WAVE];
-            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], x1, lo, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][1], x0, lo, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], x0, acc, 0, 0, 0);
-          }
-        } else {
+      for (int rs = 0; rs < 2; ++rs) {
+        f32x4 acc[2], lo[2];
 #pragma unroll
-          for (int kb = k0; kb < k0 + 8; ++kb) {
+        for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[cs][e] = lo[cs][e] = 0.0f;
+        auto khalf = [&](auto k0c) {
+          constexpr int k0 = decltype(k0c)::value;
+#pragma unroll
+          for (int kb = k0; kb < k0 + 4; ++kb) {
             bf16x8 xs[NP];
+            if constexpr ((ABL & 1) != 0) {
+              using i32x4 = __attribute__((ext_vector_type(4))) int;
+              i32x4 x = __builtin_bit_cast(i32x4, Sr[((kb * 2 + rs) * NP) * SVDJ_WAVE]);
 #pragma unroll
-            for (int i = 0; i < NP; ++i) xs[i] = Sr[(kb * NP + i) * SVDJ_WAVE];
-            lo = mfma_split<NP, 1>(qf[kb], xs, lo);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
+              for (int i = 1; i < NP; ++i)
+                x ^= __builtin_bit_cast(i32x4, Sr[((kb * 2 + rs) * NP + i) * SVDJ_WAVE]);
+#pragma unroll
+              for (int cs = 0; cs < 2; ++cs) acc[cs] = mfma16(qf[kb][cs][0], __builtin_bit_cast(bf16x8, x), acc[cs]);
+            } else if constexpr (NP == 3 && ((CH >> (k0 / 4)) & 1) != 0) {
+              xs[0] = Sr[((kb * 2 + rs) * NP + 0) * SVDJ_WAVE];
+              xs[1] = Sr[((kb * 2 + rs) * NP + 1) * SVDJ_WAVE];
+#pragma unroll
+              for (int cs = 0; cs < 2; ++cs) {
+                lo[cs] = mfma16(qf[kb][cs][0], xs[1], lo[cs]);
+                lo[cs] = mfma16(qf[kb][cs][1], xs[0], lo[cs]);
+                acc[cs] = mfma16(qf[kb][cs][0], xs[0], acc[cs]);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < NP; ++i) xs[i] = Sr[((kb * 2 + rs) * NP + i) * SVDJ_WAVE];
+#pragma unroll
+              for (int cs = 0; cs < 2; ++cs) {
+#pragma unroll
+                for (int ord = NP - 1; ord >= 1; --ord)  // products of order ord, small first
+#pragma unroll
+                  for (int a = 0; a <= ord; ++a) lo[cs] = mfma16(qf[kb][cs][a], xs[ord - a], lo[cs]);
+                acc[cs] = mfma16(qf[kb][cs][0], xs[0], acc[cs]);
+              }
+            }
+            // no scheduling across k blocks: hoisted fragment loads of later
+            // blocks pushed the T slice out of registers
+            __builtin_amdgcn_sched_barrier(0);
           }
+        };
+        if constexpr ((ABL & 4) == 0) {
+          khalf(std::integral_constant<int, 0>{});
+          khalf(std::integral_constant<int, 4>{});
         }
-      };
-      if constexpr ((ABL & 5) == 0) {
-        khalf(std::integral_constant<int, 0>{});
-        khalf(std::integral_constant<int, 8>{});
-      }
+        // 4. own raw values of this half, still in this wave's raw image R[buf]
+        //    (its refill, tile t + 2, is issued below), and the delta-form
+        //    store, in place (acc[cs] register e is own column 16 cs + 4g + e,
+        //    row 16 rs + i).  (Staging the finished tile
+        //    through R[buf] for 16-byte stores cut the compute-only time of the
+        //    32x32x16 form 1229 -> 1037 us but not the solve's:
+        //    profiles/r6_apply/ablation_vector_epilogue_rejected.jsonl.)
 #pragma unroll
-      for (int kb = 0; kb < 16 && (ABL & 5) == 1; ++kb) {
-        bf16x8 xs[NP];
-#pragma unroll
-        for (int i = 0; i < NP; ++i) xs[i] = Sr[(kb * NP + i) * SVDJ_WAVE];
-        if constexpr ((ABL & 1) != 0) {
-          using i32x4 = __attribute__((ext_vector_type(4))) int;
-          i32x4 x = __builtin_bit_cast(i32x4, xs[0]);
-#pragma unroll
-          for (int i = 1; i < NP; ++i) x ^= __builtin_bit_cast(i32x4, xs[i]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], __builtin_bit_cast(bf16x8, x), acc, 0, 0, 0);
-        } else {
-          lo = mfma_split<NP, 1>(qf[kb], xs, lo);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[kb][0], xs[0], acc, 0, 0, 0);
-        }
-      }
-      acc += lo;
-      // 4. own raw values, still in this wave's raw image R[buf] (its refill,
-      //    tile t + 2, is issued below), and the delta-form store, in place
-      //    (acc layout: register 4g + i is own column 8g + 4h + i, row c).
-      //    (Staging the finished tile through R[buf] for 16-byte stores cut
-      //    the compute-only time 1229 -> 1037 us but not the solve's:
-      //    profiles/r6_apply/ablation_vector_epilogue_rejected.jsonl.)
-      {
-        const bool isA = t < a_tiles;
-        float* const own = isA ? ownA : ownV;
-        const int ld = isA ? lda : ldv, r0 = (isA ? t : t - a_tiles) * 32;
-        const uint32_t st_off = (uint32_t)(4 * h * ld + c) + (uint32_t)r0;
-        const float* Rr = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int cs = 0; cs < 2; ++cs) {
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = Rr[(8 * g + 4 * h + i) * 32 + c];
+          for (int e = 0; e < 4; ++e) v[e] = R[eb + 512 * cs + 32 * e + 16 * rs];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float y = v[i] + acc[4 * g + i];
+          for (int e = 0; e < 4; ++e) {
+            const float y = v[e] + (acc[cs][e] + lo[cs][e]);
             if ((ABL & 2) == 0 || y == -1.2345e-30f)
-              at_u32(own + (size_t)Mfma<float>::acc_row_uni(4 * g + i) * ld, st_off) = y;
+              at_u32(own + (size_t)(16 * cs + e) * ld + 16 * rs, st_off) = y;
           }
         }
       }
@@ -2366,7 +2407,8 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       else run(std::integral_constant<int, 3>{});
     }
     // work counters of the sweep (metric words 6, 7; svdj_stop.h): MFMAs this
-    // wave issued in units of 24 (96, 72 or 48 per tile), and tiles moved
+    // wave issued in 32x32x16 units of 24 (96, 72 or 48 per tile = twice as
+    // many 16x16x32 ones), and tiles moved
     if (work && lane == 0) {
       const uint32_t per = NP == 3 ? 4u - (cheap & 1u) - ((cheap >> 1) & 1u) : 2u;
       atomicAdd(&work[0], (uint32_t)(t1 - t0) * per);
@@ -2823,7 +2865,7 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                          0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq, c.Ts[b]);
     SVDJ_LAUNCH_CHECK();
     if (lat) {  // 2 rows per thread: fp32 T, then the split pass
-      const dim3 tg(c.P / 2, 16 * 8 * 64 / kTsplitThreads);
+      const dim3 tg(c.P / 2, 8 * 8 * 2 * 64 / kTsplitThreads);
       if (mma == 2)
         hipLaunchKernelGGL((tsplit_kernel<2>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
                            c.skip1[b], c.skip2[b]);
