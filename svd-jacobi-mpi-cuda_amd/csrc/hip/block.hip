@@ -2185,7 +2185,8 @@ __global__ __launch_bounds__(kQuadTsThreads) __attribute__((amdgpu_waves_per_eu(
 apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restrict__ V, int ldv,
                      int v_tiles, const int32_t* __restrict__ pairs, int nq,
                      const bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
-                     const int32_t* __restrict__ skip2, uint32_t* __restrict__ work = nullptr) {
+                     const int32_t* __restrict__ skip2, uint32_t* __restrict__ work = nullptr,
+                     float cheap_tol = 0.001953125f) {
   using L = QuadTsLds<NP>;
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int lane = threadIdx.x & 63;
@@ -2248,7 +2249,7 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
           for (int cs = 0; cs < 2; ++cs)
 #pragma unroll
             for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf((float)qf[kb][cs][0][e]));
-        if (wave_max(mx) <= 0.001953125f) cheap |= 1u << hf;
+        if (wave_max(mx) <= cheap_tol) cheap |= 1u << hf;
       }
       cheap = __builtin_amdgcn_readfirstlane(cheap);
     }
@@ -2453,24 +2454,56 @@ __global__ __launch_bounds__(kRedThreads) void slab_reduce_kernel(const float* _
 // one workgroup (8 waves) per (quad, row chunk):
 //   * wave w LDS-DMAs column tile w (32 of the quad's 256 columns, [a b c d]
 //     order) of each 32-row slab two slabs ahead into a wave-private raw
-//     image, and splits it into 3 RNE bf16 parts in the shared A/B fragment
-//     image (lane (c, h): column c, rows 8h .. 8h+7 of a 16-row k step);
-//   * the 24 output tiles (6 products x 2 x 2 tiles of 32 x 32) are dealt 3
-//     per wave; each tile takes the 6 products of order < 3 per k step
-//     (leading product and the small ones in two accumulators), the error of
-//     a product below 2^-26 relative, like the split apply;
+//     image, and splits it into 3 RNE bf16 parts -- lane (i, g) of 16-column
+//     sub-tile s: column 16 s + i, rows 8g .. 8g+7, exactly the A and the B
+//     operand of v_mfma_f32_16x16x32_bf16 -- kept in registers and written to
+//     the shared fragment image for the other waves;
+//   * OWNER-based tiles (round 6): the 24 needed 32 x 32 output tiles are the
+//     pairs of column tiles from different blocks; each is computed by one
+//     of its two column tiles' waves (kGramPartner: every wave 3 partners), so
+//     a wave's own operand never leaves its registers and it reads only its 3
+//     partners' fragments (18 x 1 KB per slab and wave instead of 36: the
+//     round-5 form, any 3 tiles per wave with both operands from LDS, was
+//     LDS-bandwidth bound -- 142 us of 278 with one MFMA per product,
+//     profiles/r6_apply/ablation_gram.jsonl);
+//   * each 16 x 16 sub-tile takes the 6 products of order < 3 (leading product
+//     and the small ones in two accumulators), the error of a product below
+//     2^-26 relative, like the split apply;
 //   * the tiles go straight to the slab layout the consumers read: slab
 //     (pair 2q) = C_ac, (2q+1) = C_bd, then per quad C_ad, C_bc, C_ab, C_cd
-//     (the order quad_update_kernel reads), one W x W slab per row chunk.
+//     (the order quad_update_kernel reads), one W x W slab per row chunk; a
+//     tile whose owner is its slab's column block is stored transposed.
 constexpr int kGramQThreads = 512;
 struct GramQLds {
-  static constexpr int S_BYTES = 2 * 8 * 3 * SVDJ_WAVE * 16;  // 2 k steps x 8 col tiles x 3 parts
+  static constexpr int S_BYTES = 8 * 2 * 3 * SVDJ_WAVE * 16;  // 8 col tiles x 2 sub-tiles x 3 parts
   static constexpr int R_BYTES = 8 * 32 * 32 * 4;             // raw 32-row slab, wave w at 4 KB * w
   static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
 };
 static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
+// Partners of column tile w (tile t is block t >> 1 of [a b c d], half t & 1):
+// the 24 pairs of tiles from different blocks, each listed once, 3 per tile
+// (3 bits each, partner j at bits 3j).
+__device__ __forceinline__ int gram_partners(int w) {
+  constexpr int PK[8] = {2 | 3 << 3 | 4 << 6, 2 | 3 << 3 | 5 << 6, 4 | 5 << 3 | 6 << 6,
+                         4 | 5 << 3 | 7 << 6, 1 | 6 << 3 | 7 << 6, 0 | 6 << 3 | 7 << 6,
+                         0 | 1 << 3 | 3 << 6, 0 | 1 << 3 | 2 << 6};
+  int r = PK[0];
+#pragma unroll
+  for (int t = 1; t < 8; ++t) r = w == t ? PK[t] : r;
+  return r;
+}
+// Product (slab) of blocks (x, y) of [a b c d]: ac bd ad bc ab cd = 0 .. 5;
+// bit 3 set when (x, y) is the transposed order.
+__host__ __device__ constexpr int gram_product_fwd(int x, int y) {
+  return x == 0 && y == 2 ? 0 : x == 1 && y == 3 ? 1 : x == 0 && y == 3 ? 2 : x == 1 && y == 2 ? 3
+       : x == 0 && y == 1 ? 4 : x == 2 && y == 3 ? 5 : -1;
+}
+__host__ __device__ constexpr int gram_product(int x, int y) {
+  return gram_product_fwd(x, y) >= 0 ? gram_product_fwd(x, y) : 8 | gram_product_fwd(y, x);
+}
+static_assert(gram_product(2, 0) == 8 && gram_product(3, 2) == 13, "gram_product");
 // ABL (tools/micro/quad_apply_ab.hip only; production launches ABL = 0):
-// bit 0 one MFMA per output tile and k step instead of 6; bit 1 no global
+// bit 0 one MFMA per output sub-tile and slab instead of 6; bit 1 no global
 // reads (no DMA, no waits).
 template <int ABL = 0>
 __global__ __launch_bounds__(kGramQThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
@@ -2482,18 +2515,17 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
   const int q = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = lane & 31, h = lane >> 5;
+  const int i16 = lane & 15, g = lane >> 4;
   const int32_t* qp = pairs + 4 * q;  // (a, c), (b, d)
   auto blk = [&](int qb) { return qp[(qb & 1) * 2 + (qb >> 1)]; };  // [a b c d] -> block id
   const int r_begin = chunk * rows_per_chunk;
   const int r_end = min(m_pad, r_begin + rows_per_chunk);
   const int ns = (r_end - r_begin) / 32;  // rows_per_chunk and m_pad are multiples of 128
   const float* own = A + (size_t)__builtin_amdgcn_readfirstlane(blk(wave >> 1) * W + (wave & 1) * 32) * lda;
-  // products in [a b c d] block order: (x, y) and the slab each goes to
-  constexpr int PX[6] = {0, 1, 0, 1, 0, 2}, PY[6] = {2, 3, 3, 2, 1, 3};  // ac bd ad bc ab cd
+  const int pk = __builtin_amdgcn_readfirstlane(gram_partners(wave));
   // raw image [col][16-byte row chunk], chunk slot j of column col holding
   // rows 4 (j ^ (col & 7)) .. + 3: the split's reads (8 rows of one column per
-  // lane, lanes at a 128-byte column stride) then spread over all banks
+  // lane, lanes at a 128-byte column stride) then spread over the banks
   // instead of piling onto a few (35 % bank-conflict cycles unswizzled)
   auto dma = [&](int sl, int buf) {
     if constexpr ((ABL & 2) != 0) return;
@@ -2505,62 +2537,69 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
       __builtin_amdgcn_global_load_lds(own + (size_t)(8 * i + (lane >> 3)) * lda + r0 + jr,
                                        dst + i * 1024, 16, 0, 0);
   };
-  f32x16 acc[3], lo[3];
+  // [partner j][own sub-tile s][partner sub-tile s2]
+  f32x4 acc[3][2][2], lo[3][2][2];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) acc[j] = lo[j] = Mfma<float>::zero();
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[j][s][s2][e] = lo[j][s][s2][e] = 0.0f;
   auto slab = [&](int sl, auto bufc) {
     constexpr int buf = decltype(bufc)::value;
     if constexpr ((ABL & 2) != 0) {
     } else if (sl + 1 < ns) wait_vmcnt<4>();
     else wait_vmcnt<0>();
-    {  // split column tile `wave` of this slab: rows 16 kk + 8h .. + 7 of column c
+    bf16x8 xf[2][NP];
+    {  // split own column tile: sub-tile s, column 16 s + i, rows 8g .. 8g+7
       const float* R = reinterpret_cast<const float*>(lds + 2 * L::S_BYTES + buf * L::R_BYTES + wave * 4096);
       bf16x8* Sw = reinterpret_cast<bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int rc = 4 * kk + 2 * h;  // row chunks rc, rc + 1 of column c
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * (rc ^ (c & 7)));
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * ((rc + 1) ^ (c & 7)));
-        bf16x8 parts[NP];
+      for (int s = 0; s < 2; ++s) {
+        const int c = 16 * s + i16;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * ((2 * g) ^ (c & 7)));
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(R + c * 32 + 4 * ((2 * g + 1) ^ (c & 7)));
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           __bf16 pp[NP];
           split_bf16<NP>(e < 4 ? v0[e] : v1[e - 4], pp);
 #pragma unroll
-          for (int i = 0; i < NP; ++i) parts[i][e] = pp[i];
+          for (int i = 0; i < NP; ++i) xf[s][i][e] = pp[i];
         }
 #pragma unroll
-        for (int i = 0; i < NP; ++i) Sw[((kk * 8 + wave) * NP + i) * SVDJ_WAVE] = parts[i];
+        for (int i = 0; i < NP; ++i) Sw[((wave * 2 + s) * NP + i) * SVDJ_WAVE] = xf[s][i];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bf16x8* Sr = reinterpret_cast<const bf16x8*>(lds + buf * L::S_BYTES) + lane;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int j = 0; j < 3; ++j) {
+      const int yt = (pk >> (3 * j)) & 7;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int t = 3 * wave + j, pr = t >> 2, ti = (t >> 1) & 1, tj = t & 1;
-        const int cx = 2 * PX[pr] + ti, cy = 2 * PY[pr] + tj;  // column tiles
-        bf16x8 xf[NP], yf[NP];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 yf[NP];
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          xf[i] = Sr[((kk * 8 + cx) * NP + i) * SVDJ_WAVE];
-          yf[i] = Sr[((kk * 8 + cy) * NP + i) * SVDJ_WAVE];
-        }
-        if constexpr ((ABL & 1) != 0) {
-          using i32x4 = __attribute__((ext_vector_type(4))) int;
-          i32x4 xx = __builtin_bit_cast(i32x4, xf[0]) ^ __builtin_bit_cast(i32x4, xf[1]) ^
-                     __builtin_bit_cast(i32x4, xf[2]);
-          i32x4 yy = __builtin_bit_cast(i32x4, yf[0]) ^ __builtin_bit_cast(i32x4, yf[1]) ^
-                     __builtin_bit_cast(i32x4, yf[2]);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xx),
-                                                         __builtin_bit_cast(bf16x8, yy), acc[j], 0, 0, 0);
-        } else {
-          lo[j] = mfma_split<NP, 1>(xf, yf, lo[j]);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xf[0], yf[0], acc[j], 0, 0, 0);
+        for (int i = 0; i < NP; ++i) yf[i] = Sr[((yt * 2 + s2) * NP + i) * SVDJ_WAVE];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if constexpr ((ABL & 1) != 0) {
+            using i32x4 = __attribute__((ext_vector_type(4))) int;
+            i32x4 yy = __builtin_bit_cast(i32x4, yf[0]) ^ __builtin_bit_cast(i32x4, yf[1]) ^
+                       __builtin_bit_cast(i32x4, yf[2]);
+            acc[j][s][s2] = mfma16(xf[s][0], __builtin_bit_cast(bf16x8, yy), acc[j][s][s2]);
+          } else {
+#pragma unroll
+            for (int ord = NP - 1; ord >= 1; --ord)  // products of order ord, small first
+#pragma unroll
+              for (int a = 0; a <= ord; ++a) lo[j][s][s2] = mfma16(xf[s][a], yf[ord - a], lo[j][s][s2]);
+            acc[j][s][s2] = mfma16(xf[s][0], yf[0], acc[j][s][s2]);
+          }
         }
       }
+    }
     if (sl + 2 < ns) dma(sl + 2, buf);
   };
   if (ns > 0) dma(0, 0);
@@ -2569,16 +2608,29 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
     slab(sl, std::integral_constant<int, 0>{});
     if (sl + 1 < ns) slab(sl + 1, std::integral_constant<int, 1>{});
   }
-  // the wave's three tiles straight to their slabs
+  // register e of lane (i, g) of sub-tile (s, s2) = C[own column 16 s + 4g + e]
+  // [partner column 16 s2 + i]; straight to the slabs
+  const int bx = wave >> 1;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int t = 3 * wave + j, pr = t >> 2, ti = (t >> 1) & 1, tj = t & 1;
+    const int yt = (pk >> (3 * j)) & 7, by = yt >> 1;
+    const int code = gram_product(bx, by), pr = code & 7;
     const size_t sidx = pr < 2 ? (size_t)(2 * q + pr) * nchunk + chunk
                                : (size_t)P * nchunk + ((size_t)q * 4 + (pr - 2)) * nchunk + chunk;
-    float* out = slabs + sidx * (W * W) + (ti * 32) * W + tj * 32 + c;
-    const f32x16 v = acc[j] + lo[j];
+    float* out = slabs + sidx * (W * W);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) out[Mfma<float>::acc_row(e, lane) * W] = v[e];
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const f32x4 v = acc[j][s][s2] + lo[j][s][s2];
+        const int xr = 32 * (wave & 1) + 16 * s + 4 * g, yc = 32 * (yt & 1) + 16 * s2 + i16;
+        if (code & 8) {  // slab rows are the partner's block
+          *reinterpret_cast<f32x4*>(out + yc * W + xr) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) out[(xr + e) * W + yc] = v[e];
+        }
+      }
   }
 }
 
@@ -2840,8 +2892,12 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     // (16384^2 rank plans, ms per sweep: P = 4 76.9 -> 72.5, P = 2 131.9 ->
     // 130.0, profiles/r5_quad2/reduce)
     const bool lat = c.P < 64;
+    static const int qb1 = svdj_debug_knob("qb1_threads", 512);  // A/B only (svdj_debug.h)
     if (lat)
       hipLaunchKernelGGL((qbuild_quad_kernel<1, 2, QBT>), dim3(c.P, 128 / (2 * QBW)), dim3(QBT), 0,
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+    else if (qb1 == 512)  // two workgroups per pair: all CUs busy at 128 pairs
+      hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 512>), dim3(c.P, 128 / (R * 8)), dim3(512), 0,
                          c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
     else
       hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
@@ -2971,10 +3027,12 @@ static int launch_apply(const Chain<T>& c, int s, int mma, uint32_t* metric) {
       // T-stationary persistent apply (apply_quad_ts_kernel)
       const int nq = c.P / 2, at = c.m_pad / 32, vt = c.V ? c.n_v / 32 : 0;
       uint32_t* work = metric ? metric + 6 : nullptr;
+      // cheap k halves: |T - I| <= 2^-9 (A/B only: SVDJ_DEBUG cheap_log2, svdj_debug.h)
+      static const float cheap_tol = ldexpf(1.0f, -svdj_debug_knob("cheap_log2", 9));
       if (mma == 1)
         hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
-                           c.skip2[b], work);
+                           c.skip2[b], work, cheap_tol);
       else
         hipLaunchKernelGGL((apply_quad_ts_kernel<2>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],

@@ -5,10 +5,15 @@
 //     merge=0|1            one-GPU merged issue of the two chains forced off/on
 //                          (world 1 only, both engines: svdj_dist_issue_rules,
 //                          parallel/distributed.py choose_merged)
+//     merge_dist=1         Python engine, P > 1: the merged issue with exchanges
+//                          (PipelineExecutor.run(merge=True))
 //     gram_chunks=N        row chunks of the single-step Gram (make_geometry)
 //     quad_gram_chunks=N   row chunks of the quad Gram (quad_geometry)
 //     stream_order=B       row-chunk dispatch order: bit 0 cross Gram chunks
 //                          last-first, bit 1 the apply's V chunks before A's
+//     cheap_log2=K         quad apply: first-order-only k halves where
+//                          |T - I| <= 2^-K (default 9)
+//     qb1_threads=N        phase-1 quad Q build workgroup size (1024 or 512)
 //
 // svdj_debug_knob returns the value of `key`, or `dflt` when SVDJ_DEBUG is
 // unset or does not name it.  Host code only; callers cache the result.

@@ -338,9 +338,11 @@ class DistributedBlockJacobi(Solver):
         # pairs keep the overlapped chains (8192^2 merged +10 %); quad steps
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
         # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_DEBUG merge=0/1
-        # overrides; with exchanges merging was slower at every P.
-        merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
-                                                                    k, quad)
+        # overrides; with exchanges merging was slower at every P (SVDJ_DEBUG
+        # merge_dist=1 selects it there, A/B only, this engine only).
+        merged = pipelined and dev.type == "cuda" and (
+            choose_merged(P if comm.distributed else 1, k, quad)
+            or (comm.distributed and debug_knob("merge_dist") == 1))
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
