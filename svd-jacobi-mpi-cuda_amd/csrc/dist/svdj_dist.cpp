@@ -673,10 +673,12 @@ extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k
   if (quad_mode < 0 || quad_mode > 2) return fail(-2, "quad %d (0 auto, 1 on, 2 off)", quad_mode);
   if (quad_mode == 1 && !quad_ok)
     return fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
+  // models/block.py choose_quad, parallel/distributed.py choose_merged
   const int hk = k / 2;
-  *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && (hk >= 32 || (hk >= 16 && m_pad >= 16384))));
+  *quad = quad_ok && (quad_mode == 1 ||
+                      (quad_mode == 0 && (hk >= 32 || (hk >= 16 && (m_pad >= 16384 || world == 1)))));
   const int force = svdj_debug_knob("merge", -1);  // A/B only (svdj_debug.h), world 1 only
-  *merged = world == 1 && (force >= 0 ? force == 1 : hk >= (*quad ? 32 : 64));
+  *merged = world == 1 && (force >= 0 ? force == 1 : hk >= (*quad ? 16 : 64));
   return 0;
 }
 

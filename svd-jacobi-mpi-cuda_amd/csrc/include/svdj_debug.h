@@ -12,8 +12,9 @@
 //     stream_order=B       row-chunk dispatch order: bit 0 cross Gram chunks
 //                          last-first, bit 1 the apply's V chunks before A's
 //     cheap_log2=K         quad apply: first-order-only k halves where
-//                          |T - I| <= 2^-K (default 9)
+//                          |T - I| <= 2^-K (default 7)
 //     qb1_threads=N        phase-1 quad Q build workgroup size (1024 or 512)
+//     upd_threads=N        quad_update_kernel workgroup size (256 or 512)
 //
 // svdj_debug_knob returns the value of `key`, or `dflt` when SVDJ_DEBUG is
 // unset or does not name it.  Host code only; callers cache the result.

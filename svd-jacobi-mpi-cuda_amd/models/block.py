@@ -99,10 +99,15 @@ def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int
     596, 65536^2 P=8 1749 vs 2112; with 16 pairs: 16384^2 P=4 78.3 vs 85.0,
     32768^2 P=8 223 vs 324, but 8192^2 P=2 28.5 vs 27.7 and 4096^2 on one GPU
     158 vs 136 ms (short columns: the longer EVD chain is exposed); with 8
-    pairs quad steps lose (16384^2 P=8 57 vs 43)."""
+    pairs quad steps lose (16384^2 P=8 57 vs 43).  Round 6 (profiles/r6_issue):
+    on ONE GPU with 16 pairs the quad steps win once the two chains are
+    merged into single launches (choose_merged) -- 4096^2 123.5 ms merged quad
+    vs 127.1 merged single steps vs 135.4 two chains -- so there the row rule
+    does not apply; 16384^2 P=8 (8 pairs) stays without: 52.8 ms per sweep
+    quad, 50.6 merged-with-exchanges quad, 51.9 merged single, 43.1 default."""
     if not quad_supported(dtype, W, mma, k):
         return False
-    return k // 2 >= 32 or (k // 2 >= 16 and m_pad >= 16384)
+    return k // 2 >= 32 or (k // 2 >= 16 and (m_pad >= 16384 or P == 1))
 
 
 def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int,

@@ -48,7 +48,7 @@ from .schedule import distributed_sweep_plan, tournament
 
 def choose_merged(P: int, k: int, quad: bool) -> bool:
     """One-GPU merged issue (PipelineExecutor.run_merged) for k W-blocks per
-    super-block: from 64 pairs per chain step, 32 with quad steps (measured:
+    super-block: from 64 pairs per chain step, 16 with quad steps (measured:
     see the comment at its use in DistributedBlockJacobi._solve).  The
     reference's single-process path rotates one pair per launch
     (main.cu:727-758); this is the opposite end: all of a step's pairs of
@@ -60,7 +60,7 @@ def choose_merged(P: int, k: int, quad: bool) -> bool:
     force = debug_knob("merge")
     if force is not None:
         return force == 1
-    return k // 2 >= (32 if quad else 64)
+    return k // 2 >= (16 if quad else 64)
 
 
 class DistributedBlockJacobi(Solver):
@@ -337,7 +337,8 @@ class DistributedBlockJacobi(Solver):
         # two-chain solve, the Gram keeps the chunking).  Single steps of 32
         # pairs keep the overlapped chains (8192^2 merged +10 %); quad steps
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
-        # 39.4 -> 36.9 ms, profiles/r5_quad2).  SVDJ_DEBUG merge=0/1
+        # 39.4 -> 36.9 ms, profiles/r5_quad2), and so do quad steps of 16
+        # pairs (4096^2 135.4 -> 123.5 ms, profiles/r6_issue).  SVDJ_DEBUG merge=0/1
         # overrides; with exchanges merging was slower at every P (SVDJ_DEBUG
         # merge_dist=1 selects it there, A/B only, this engine only).
         merged = pipelined and dev.type == "cuda" and (

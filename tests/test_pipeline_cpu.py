@@ -406,8 +406,9 @@ def test_native_issue_rules_match_python(monkeypatch):
 def test_quad_and_merge_rules_pin_the_measured_choices():
     """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
     quad steps on 1, 2 and 4 GPUs (64 / 32 / 16 pairs per chain step, 16384
-    rows) but not on 8 (8 pairs); 4096^2 on one GPU does not (16 pairs on
-    4096-row columns); 8192^2 on one GPU does, merged (32 pairs)."""
+    rows) but not on 8 (8 pairs); 8192^2 on one GPU does, merged (32 pairs);
+    4096^2 on one GPU does too, merged (16 pairs: round 6, profiles/r6_issue),
+    but 8192^2 on two GPUs (16 pairs on 8192-row columns) does not."""
     import torch
 
     from svdj.models.block import resolve_quad
@@ -423,7 +424,8 @@ def test_quad_and_merge_rules_pin_the_measured_choices():
     assert plan(16384, 2) == (True, False)
     assert plan(16384, 4) == (True, False)
     assert plan(16384, 8) == (False, False)
-    assert plan(4096, 1) == (False, False)
+    assert plan(4096, 1) == (True, True)
+    assert plan(8192, 2) == (False, False)
     assert plan(8192, 1) == (True, True)
     assert plan(32768, 8) == (True, False)
     assert not resolve_quad("auto", torch.float64, 64, "native", 128, 1, 16384)
