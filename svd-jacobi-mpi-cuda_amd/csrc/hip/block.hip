@@ -424,13 +424,15 @@ __device__ __forceinline__ bool needs_rotation(double gpp, double gqq, double gp
 }
 // Effective sine of a rotation for the second-order stop test
 // (svdj_stop.h): |s| times the larger ratio of the two columns' norms after
-// it (d = squared norms); 0 for no rotation.
+// it (d = squared norms); 0 for no rotation.  Hardware rcp / sqrt (~1 ulp:
+// a stop-test statistic; the IEEE division and square root were ~30
+// instructions on the EVD solver lane's step).
 template <typename T>
 __device__ __forceinline__ float eff_sine(T s, T dp, T dq) {
   if (s == T(0)) return 0.0f;
   const float a = (float)fabs(dp), b = (float)fabs(dq);
   const float lo = fminf(a, b), hi = fmaxf(a, b);
-  return lo > 0.0f ? fabsf((float)s) * sqrtf(hi / lo) : 1.0f;
+  return lo > 0.0f ? fabsf((float)s) * __builtin_amdgcn_sqrtf(hi * __builtin_amdgcn_rcpf(lo)) : 1.0f;
 }
 // The negligible-column floor of this solve (metric[2..3], a double).
 template <typename T>
@@ -1167,7 +1169,11 @@ template <int W>
 __host__ __device__ constexpr int cross_threads() { return W == 64 ? 1024 : 512; }
 constexpr int kCrossMaxInner = 4;  // inner sweeps whose rotation records fit the workspace
 
-template <typename T, int W>
+// ABL (tools/micro/evd_bench.hip only; production launches ABL = 0): bit 0
+// no fp64 rotation records; bit 1 waves >= 1 skip their coupling updates
+// (barriers kept); bit 2 the solver lane skips the rotation (c = 1, s = 0);
+// bit 3 the solver lane skips its LDS coupling read and write.
+template <typename T, int W, int ABL = 0>
 __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     const int32_t* __restrict__ pairs, const T* __restrict__ slabs, int nchunk,
     T* __restrict__ D, Pair2<double>* __restrict__ rec, int32_t* __restrict__ nsteps,
@@ -1289,24 +1295,30 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
                 // recorded; the look-ahead rotation solved in the final phase
                 // is never used)
   // second-order stop test (svdj_stop.h): largest effective sine and count
-  // of the rotations applied (recorded); rse: effective sine of the latest
-  // solved rotation
-  float smax = 0.0f, rse = 0.0f;
+  // of the rotations applied (recorded); the effective sine of the latest
+  // solved rotation is formed when it is recorded, off the solve chain
+  float smax = 0.0f;
   uint32_t rcount = 0;
   auto solve = [&](T dx, T dy, T g, bool& rot) {
     T c, sn, t;
-    rot = rotation_fast(dx, dy, g, tol, absmode, nfloor, c, sn, t);
+    if constexpr ((ABL & 4) != 0) {
+      rot = false;
+      c = T(1);
+      sn = t = T(0);
+    } else {
+      rot = rotation_fast(dx, dy, g, tol, absmode, nfloor, c, sn, t);
+    }
     rc = c;
     rs = sn;
     rt = t;
     rdx = dx - t * g;
     rdy = dy + t * g;
-    rse = eff_sine(sn, rdx, rdy);
     pend = rot ? T(0) : g;
   };
-  auto record = [&](int step) {
-    smax = fmaxf(smax, rse);
+  auto record = [&](int step) {  // before the next solve: rs, rdx, rdy still its inputs'
+    smax = fmaxf(smax, eff_sine(rs, rdx, rdy));
     rcount += rs != T(0) ? 1u : 0u;
+    if constexpr ((ABL & 1) != 0) return;
     double c64, s64;
     if constexpr (sizeof(T) == 8) {
       c64 = rc;
@@ -1337,7 +1349,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     const bool last = st + 1 == W;  // this phase solves step 0 of the next inner sweep
     if (wave == 0) {
       // neighbours' values (slot a+1, a+2) by lane rotates; E_t[a][a+2] from LDS
-      const T g2 = solver ? Eb[b][a * W + (a + 2) % W] : T(0);
+      const T g2 = solver && (ABL & 8) == 0 ? Eb[b][a * W + (a + 2) % W] : T(0);
       // fp64 record of step gs (solved in the previous phase) while the LDS
       // read is in flight: off the barrier-to-barrier critical path
       if (solver) record(gs);
@@ -1352,7 +1364,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
         const T n1_1 = cc1 * h1 - ss1 * g1;  // E_{t+1}[a+1][a-1]
         const T n0_2 = cc2 * g2 - ss2 * h2;  // E_{t+1}[a][a+1]
         const T n1_2 = cc2 * h2 - ss2 * g2;  // E_{t+1}[a+2][a-1] (a d = 3 group's input)
-        Eb[nb][((a + 2) % W) * W + (a + W - 1) % W] = n1_2;
+        if constexpr ((ABL & 8) == 0) Eb[nb][((a + 2) % W) * W + (a + W - 1) % W] = n1_2;
         dx_out = rdx;
         dy_out = rdy;
         pend_prev = pend;
@@ -1369,7 +1381,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
         racc = racc_next;
         racc_next = 0;
       }
-    } else {
+    } else if constexpr ((ABL & 2) == 0) {
       T e0[2], e1[2];
       T2 ri[2], rp[2];
 #pragma unroll
@@ -1903,26 +1915,27 @@ __global__ __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(2
 
 // Q of an EVD pair (phase 1, rows of the pair, output fp64 T1) or the quad's
 // T (phase 2: rows of all 4 blocks, starting from the phase-1 transforms,
-// output fp32).  Same row-parallel rotation loop as qbuild_kernel; a skipped
-// pair contributes the identity (phase 1 writes it: T1 is read by update and
-// phase 2 even when its pair did not rotate).
+// output T - I split into NP bf16 parts).  Same row-parallel rotation loop as
+// qbuild_kernel; a skipped pair contributes the identity (phase 1 writes it:
+// T1 is read by update and phase 2 even when its pair did not rotate).
 // First element of the split T - I fragment (quad q, 32-row k block kb, 32-column
 // tile ct, 16-column sub-tile cs) in the apply's A-operand layout
-// (tsplit_kernel, apply_quad_ts_kernel): NP parts of SVDJ_WAVE bf16x8 each.
+// (apply_quad_ts_kernel): NP parts of SVDJ_WAVE bf16x8 each; element e of lane
+// 16g + i = (T - I)[32 kb + 8g + e][32 ct + 16 cs + i].
 __host__ __device__ constexpr size_t ts_frag(int q, int kb, int ct, int cs, int np) {
   return ((((size_t)q * 8 + kb) * 8 + ct) * 2 + cs) * np * SVDJ_WAVE;
 }
 
-// NP > 0 (phase 2 with R = 8): instead of the fp32 T, T - I is written
-// straight in the apply's split-bf16 fragment layout (what tsplit_kernel
-// makes from T): a thread's 8 rows k0 .. k0 + 7 of one column are exactly one
-// A-operand fragment (k block k0 / 32, lane group (k0 / 8) & 3).
+// Phase 2 writes T - I straight in the apply's split-bf16 fragment layout
+// (round 6; a separate split pass over an fp32 T before): a thread's R rows
+// k0 .. k0 + R - 1 of one column are elements k0 % 8 .. of one A-operand
+// fragment (k block k0 / 32, lane group (k0 / 8) & 3).
 template <int PHASE, int R, int NT, int NP = 0>
 __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
     const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
-    const int32_t* __restrict__ skip, double* __restrict__ T1, float* __restrict__ Tq,
-    bf16x8* __restrict__ Ts = nullptr) {
-  static_assert(NP == 0 || (PHASE == 2 && R == 8), "direct split T: phase 2, 8 rows per thread");
+    const int32_t* __restrict__ skip, double* __restrict__ T1, bf16x8* __restrict__ Ts = nullptr) {
+  static_assert(PHASE == 1 ? NP == 0 : ((NP == 2 || NP == 3) && (R == 2 || R == 4 || R == 8)),
+                "phase 2: split T - I, 2 / 4 / 8 rows per thread");
   constexpr int W = 64, N = 2 * W, QN = 4 * W;
   constexpr int WAVES = NT / SVDJ_WAVE;
   static_assert((PHASE == 1 ? N : QN) % (R * WAVES) == 0, "row cover");
@@ -1982,34 +1995,29 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
       qo[(size_t)(k0 + i) * N + a] = qx[i];
       qo[(size_t)(k0 + i) * N + W + yr] = qy[i];
     }
-  } else if constexpr (NP == 0) {
-    float* qo = Tq + (size_t)q * QN * QN;
+  } else {  // element e of lane 16g + i of fragment (kb, ct, cs) = (T - I)[32 kb +
+            // 8g + e][32 ct + 16 cs + i]; R < 8 rows per thread fill elements
+            // k0 % 8 .. + R - 1 of the fragment
+    using bfR = __attribute__((ext_vector_type(R))) __bf16;
     const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      qo[(size_t)(k0 + i) * QN + xc] = (float)qx[i];
-      qo[(size_t)(k0 + i) * QN + yc] = (float)qy[i];
-    }
-  } else {  // tsplit_kernel's layout: element e of lane 16g + i of fragment (kb, ct, cs)
-            // = (T - I)[32 kb + 8g + e][32 ct + 16 cs + i]
-    const int xc = (j == 0 ? 0 : W) + a, yc = (j == 0 ? 3 * W : 2 * W) + yr;
-    const int kb = k0 >> 5, gg = (k0 >> 3) & 3;
+    const int kb = k0 >> 5, gg = (k0 >> 3) & 3, e0 = k0 & 7;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const int col = side ? yc : xc;
-      bf16x8 parts[NP];
+      bfR parts[NP];
 #pragma unroll
       for (int e = 0; e < R; ++e) {
         __bf16 pp[NP];
-        // T rounded to fp32 first (the T the tsplit path splits), then T - I
+        // T rounded to fp32 first, then T - I (exact: |T| <= 1)
         const float t = (float)(side ? qy[e] : qx[e]) - (k0 + e == col ? 1.0f : 0.0f);
         split_bf16<NP>(t, pp);
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) parts[pi][e] = pp[pi];
       }
-      bf16x8* dst = Ts + ts_frag(q, kb, col >> 5, (col >> 4) & 1, NP) + (col & 15) + 16 * gg;
+      __bf16* dst = reinterpret_cast<__bf16*>(Ts + ts_frag(q, kb, col >> 5, (col >> 4) & 1, NP) +
+                                              (col & 15) + 16 * gg) + e0;
 #pragma unroll
-      for (int pi = 0; pi < NP; ++pi) dst[pi * SVDJ_WAVE] = parts[pi];
+      for (int pi = 0; pi < NP; ++pi) *reinterpret_cast<bfR*>(dst + pi * SVDJ_WAVE * 8) = parts[pi];
     }
   }
 }
@@ -2111,37 +2119,6 @@ __global__ __launch_bounds__(NT) void quad_update_kernel(
     for (int e = 0; e < M::NACC; ++e)
       out[(wave * 32 + M::acc_row(e, lane)) * W + 32 * oj + li] = acc[e];
   }
-}
-
-// T - I of every quad split into NP bf16 parts (split_bf16), in the A-operand
-// order of v_mfma_f32_16x16x32_bf16: entry [q][kb][ct][cs][part][lane (i, g)]
-// element e = (T - I)[32 kb + 8g + e][32 ct + 16 cs + i], lane = 16g + i.
-// One thread per fragment; skipped quads are left alone (the apply skips them
-// too).  (qbuild_quad_kernel<2, 8, ., NP> writes the same layout directly.)
-constexpr int kTsplitThreads = 256;
-template <int NP>
-__global__ __launch_bounds__(kTsplitThreads) void tsplit_kernel(
-    const float* __restrict__ Tq, bf16x8* __restrict__ Ts, const int32_t* __restrict__ skip1,
-    const int32_t* __restrict__ skip2) {
-  constexpr int QN = 256;
-  const int q = blockIdx.x;
-  if (skip1[2 * q] && skip1[2 * q + 1] && skip2[2 * q] && skip2[2 * q + 1]) return;
-  const int idx = blockIdx.y * kTsplitThreads + threadIdx.x;  // < 8 * 8 * 2 * 64
-  const int kb = idx >> 10, ct = (idx >> 7) & 7, cs = (idx >> 6) & 1, lane = idx & 63;
-  const int col = ct * 32 + cs * 16 + (lane & 15), k0 = kb * 32 + 8 * (lane >> 4);
-  const float* src = Tq + (size_t)q * QN * QN + col;
-  bf16x8 parts[NP];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = k0 + e;
-    __bf16 p[NP];
-    split_bf16<NP>(src[(size_t)k * QN] - (k == col ? 1.0f : 0.0f), p);
-#pragma unroll
-    for (int i = 0; i < NP; ++i) parts[i][e] = p[i];
-  }
-  bf16x8* dst = Ts + ts_frag(q, kb, ct, cs, NP) + lane;
-#pragma unroll
-  for (int i = 0; i < NP; ++i) dst[i * SVDJ_WAVE] = parts[i];
 }
 
 // [a b c d] <- [a b c d] T, T-STATIONARY (round 5; 16x16x32 MFMAs round 6).
@@ -2740,8 +2717,9 @@ static Geometry make_geometry(int W, int P, int m_pad, int n_v, int mma = 0) {
 static size_t rup256(size_t b) { return (b + 255) / 256 * 256; }
 // Quad-step scratch (fp32 W = 64, only when the step list has quad steps):
 // the 3P Gram slabs, T1 (fp64 Q of the P step-s pairs), the step-(s+1)
-// couplings, T (P/2 quads x 256 x 256 fp32), double-buffered split T (3 bf16
-// parts = 1.5 x T each) and the skip flags of both EVDs (chain_init's layout).
+// couplings, the double-buffered split T - I (P/2 quads x 256 x 256 in 3
+// bf16 parts = 1.5 x an fp32 T each) and the skip flags of both EVDs
+// (chain_init's layout).
 static bool has_quad(int esize, int W) { return esize == 4 && W == 64; }
 static size_t quad_bytes(int P, int m_pad) {
   Geometry g;
@@ -2752,7 +2730,7 @@ static size_t quad_bytes(int P, int m_pad) {
   return rup256((size_t)3 * P * g.qgch * W * W * sizeof(float)) +
          rup256((size_t)3 * P * W * W * sizeof(float)) +
          rup256((size_t)P * 4 * W * W * sizeof(double)) + rup256((size_t)P * W * W * sizeof(float)) +
-         4 * tstride + 4 * kstride;
+         3 * tstride + 4 * kstride;
 }
 static bool has_quad_steps(const int32_t* modes, int steps) {
   for (int s = 0; modes && s < steps; ++s)
@@ -2794,7 +2772,6 @@ struct Chain {
   float* qred;  // the 3P Grams summed over their row chunks (when qgch > 4)
   double* T1;
   float* upd;
-  float* Tq;
   bf16x8* Ts[2];
   int32_t* skip1[2];
   int32_t* skip2[2];
@@ -2845,7 +2822,6 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   c.qred = nullptr;
   c.T1 = nullptr;
   c.upd = nullptr;
-  c.Tq = nullptr;
   c.Ts[0] = c.Ts[1] = nullptr;
   c.skip1[0] = c.skip1[1] = c.skip2[0] = c.skip2[1] = nullptr;
   if (quad) {
@@ -2858,9 +2834,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
     c.upd = (float*)w;
     w += rup256((size_t)P * W * W * sizeof(float));
     const size_t tstride = rup256((size_t)(P / 2 > 0 ? P / 2 : 1) * 16 * W * W * sizeof(float));
-    c.Tq = (float*)w;
-    w += tstride;
-    c.Ts[0] = (bf16x8*)w;  // 3 bf16 parts = 1.5 x the fp32 size
+    c.Ts[0] = (bf16x8*)w;  // 3 bf16 parts = 1.5 x the fp32 size of T
     c.Ts[1] = (bf16x8*)(w + 3 * tstride / 2);
     w += 3 * tstride;
     c.skip1[0] = (int32_t*)w;
@@ -2912,15 +2886,16 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     static const int qb1 = svdj_debug_knob("qb1_threads", 512);  // A/B only (svdj_debug.h)
     if (lat)
       hipLaunchKernelGGL((qbuild_quad_kernel<1, 2, QBT>), dim3(c.P, 128 / (2 * QBW)), dim3(QBT), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1);
     else if (qb1 == 512)  // two workgroups per pair: all CUs busy at 128 pairs
       hipLaunchKernelGGL((qbuild_quad_kernel<1, R, 512>), dim3(c.P, 128 / (R * 8)), dim3(512), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1);
     else
       hipLaunchKernelGGL((qbuild_quad_kernel<1, R, QBT>), dim3(c.P, 128 / (R * QBW)), dim3(QBT), 0,
-                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1, (float*)nullptr);
+                         c.st, c.rec, c.nsteps, c.skip1[b], c.T1);
     SVDJ_LAUNCH_CHECK();
-    static const int updt = svdj_debug_knob("upd_threads", 256);  // A/B only (svdj_debug.h)
+    // 512 threads: 16384^2 -27 ms, 4096^2 -1 ms against 256 (profiles/r6_chain)
+    static const int updt = svdj_debug_knob("upd_threads", 512);  // A/B only (svdj_debug.h)
     if (updt == 512)
       hipLaunchKernelGGL(quad_update_kernel<512>, dim3(c.P, 2), dim3(512), 0, c.st,
                          gs + (size_t)c.P * gn * 64 * 64, gn, c.T1, c.upd);
@@ -2932,26 +2907,20 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
                        pr1, c.upd, 1, c.D, c.rec, c.nsteps, c.skip2[b], (float)tol, absmode,
                        max_inner, metric);
     SVDJ_LAUNCH_CHECK();
-    if (lat)
-      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, QBT>), dim3(c.P, 256 / (2 * QBW)), dim3(QBT), 0,
-                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq);
-    else if (mma == 2)  // 8 rows per thread: the split T is written directly (no tsplit pass)
+    // the split T is written directly (no tsplit pass)
+    if (lat && mma == 2)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, QBT, 2>), dim3(c.P, 256 / (2 * QBW)), dim3(QBT), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Ts[b]);
+    else if (lat)
+      hipLaunchKernelGGL((qbuild_quad_kernel<2, 2, QBT, 3>), dim3(c.P, 256 / (2 * QBW)), dim3(QBT), 0,
+                         c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Ts[b]);
+    else if (mma == 2)
       hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT, 2>), dim3(c.P, 256 / (R * QBW)), dim3(QBT),
-                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq, c.Ts[b]);
+                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Ts[b]);
     else
       hipLaunchKernelGGL((qbuild_quad_kernel<2, R, QBT, 3>), dim3(c.P, 256 / (R * QBW)), dim3(QBT),
-                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Tq, c.Ts[b]);
+                         0, c.st, c.rec, c.nsteps, c.skip2[b], c.T1, c.Ts[b]);
     SVDJ_LAUNCH_CHECK();
-    if (lat) {  // 2 rows per thread: fp32 T, then the split pass
-      const dim3 tg(c.P / 2, 8 * 8 * 2 * 64 / kTsplitThreads);
-      if (mma == 2)
-        hipLaunchKernelGGL((tsplit_kernel<2>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
-                           c.skip1[b], c.skip2[b]);
-      else
-        hipLaunchKernelGGL((tsplit_kernel<3>), tg, dim3(kTsplitThreads), 0, c.st, c.Tq, c.Ts[b],
-                           c.skip1[b], c.skip2[b]);
-      SVDJ_LAUNCH_CHECK();
-    }
     return 0;
   } else {
     (void)c; (void)s; (void)tol; (void)absmode; (void)max_inner; (void)metric; (void)mma;

@@ -2,7 +2,8 @@
 // launch of P pairs (the block step's middle kernel) in isolation, for the
 // bipartite LDS kernel (mode 2) and the cross-only kernel (mode 3).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I<csrc/include> -I<csrc/hip> \
-//         tools/micro/evd_bench.hip -o evd_bench
+//         -c tools/micro/evd_bench.hip -o evd_bench.o
+//   hipcc --offload-arch=gfx950 evd_bench.o <lib/obj/post.o> -o evd_bench
 //   ./evd_bench P nchunk reps      (prints microseconds per launch)
 #include "block.hip"
 
@@ -10,7 +11,6 @@
 #include <cstdlib>
 #include <vector>
 
-void svdj::set_error(const char* fmt, ...) { (void)fmt; }
 
 template <typename K>
 static double time_it(K launch, int reps) {
@@ -77,5 +77,24 @@ int main(int argc, char** argv) {
   }, reps);
   std::printf("P %d nchunk %d: bipartite %.2f us  cross evd %.2f us  cross evd+qbuild %.2f us\n",
               P, nchunk, tb, tc, tq);
+#ifdef EVD_ABL
+  // evd_cross_kernel ablations (its ABL flags): where a step's time goes
+  auto abl = [&](auto ablc, const char* what) {
+    constexpr int A = decltype(ablc)::value;
+    reset();
+    const double t = time_it([&]() {
+      hipLaunchKernelGGL((svdj::evd_cross_kernel<float, W, A>), dim3(P), dim3(svdj::cross_threads<W>()), 0,
+                         nullptr, dp, dsl, nchunk, dD, drec, dns, dsk, 1e-6f, 0, 1, dm);
+    }, reps);
+    std::printf("  abl %2d %-44s %.2f us\n", A, what, t);
+  };
+  abl(std::integral_constant<int, 1>{}, "no fp64 records");
+  abl(std::integral_constant<int, 2>{}, "waves >= 1 idle");
+  abl(std::integral_constant<int, 4>{}, "no rotation solve");
+  abl(std::integral_constant<int, 8>{}, "solver lane: no LDS coupling traffic");
+  abl(std::integral_constant<int, 3>{}, "records off, waves >= 1 idle");
+  abl(std::integral_constant<int, 7>{}, "records off, idle, no solve");
+  abl(std::integral_constant<int, 15>{}, "all off (barriers, DPP, bookkeeping)");
+#endif
   return 0;
 }
