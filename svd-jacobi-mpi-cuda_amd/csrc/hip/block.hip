@@ -448,7 +448,9 @@ __device__ __forceinline__ bool rotation_fast(float gpp, float gqq, float gpq, f
                                               int absmode, float floor, float& c, float& s,
                                               float& t) {
   const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode, floor);
-  const float g = rot ? gpq : 1.0f;
+  // not `rot ? gpq : 1`: the rotation does not wait for the test (two
+  // independent chains; a non-rotation is selected away below)
+  const float g = gpq != 0.0f ? gpq : 1.0f;
   const float tau = (gqq - gpp) * __builtin_amdgcn_rcpf(2.0f * g);
   const float at = fabsf(tau);
   const float t_big = 0.5f * __builtin_amdgcn_rcpf(at);
@@ -463,7 +465,7 @@ __device__ __forceinline__ bool rotation_fast(double gpp, double gqq, double gpq
                                               int absmode, double floor, double& c, double& s,
                                               double& t) {
   const bool rot = needs_rotation(gpp, gqq, gpq, tol, absmode, floor);
-  const double g = rot ? gpq : 1.0;
+  const double g = gpq != 0.0 ? gpq : 1.0;
   const double tau = (gqq - gpp) / (2.0 * g);
   const double at = fabs(tau);
   const double tt = at > 1e150 ? 0.5 / at : 1.0 / (at + sqrt(fma(tau, tau, 1.0)));
@@ -1160,23 +1162,26 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 //   * waves 1.. hold d = 3..W/2 in LDS (row stride W, bank-conflict-free),
 //     two diagonals per wave; the d = 2 / d = 3 values cross through LDS.
 // ONE barrier per step.  The kernel does not accumulate Q: every step's
-// rotations go to global memory as fp64 (c, s) records, and qbuild_kernel
-// forms Q = J_0 J_1 ... row-parallel on many CUs (rows of Q evolve
-// independently).  Measured in isolation (tools/micro/evd_bench.hip, 8
+// rotations go to global memory as tangent records, and qbuild_kernel forms
+// the fp64 (c, s) and Q = J_0 J_1 ... row-parallel on many CUs (rows of Q
+// evolve independently).  Measured in isolation (tools/micro/evd_bench.hip, 8
 // pairs, W = 64): register Q accumulation and the solve chain made the
-// per-step time ~2000 cycles; the G update itself was not the limit.
+// per-step time ~2000 cycles; the G update itself was not the limit.  Round
+// 6 ablations (profiles/r6_evd): of 33 us per launch, 14 us are barriers,
+// lane rotates and bookkeeping; the fp64 (c, s) of each record cost 3.8 us
+// on the solver lane (now formed by the Q builds), the rotation solve 6 us.
 template <int W>
 __host__ __device__ constexpr int cross_threads() { return W == 64 ? 1024 : 512; }
 constexpr int kCrossMaxInner = 4;  // inner sweeps whose rotation records fit the workspace
 
 // ABL (tools/micro/evd_bench.hip only; production launches ABL = 0): bit 0
-// no fp64 rotation records; bit 1 waves >= 1 skip their coupling updates
+// no rotation records; bit 1 waves >= 1 skip their coupling updates
 // (barriers kept); bit 2 the solver lane skips the rotation (c = 1, s = 0);
 // bit 3 the solver lane skips its LDS coupling read and write.
 template <typename T, int W, int ABL = 0>
 __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     const int32_t* __restrict__ pairs, const T* __restrict__ slabs, int nchunk,
-    T* __restrict__ D, Pair2<double>* __restrict__ rec, int32_t* __restrict__ nsteps,
+    T* __restrict__ D, T* __restrict__ rec, int32_t* __restrict__ nsteps,
     int32_t* __restrict__ skip, T tol, int absmode, int max_inner, uint32_t* __restrict__ metric) {
   static_assert(W == 32 || W == 64, "cross EVD: W = 32 or 64");
   constexpr int NT = cross_threads<W>();
@@ -1289,7 +1294,7 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
   T g1 = T(0);              // E_t[a][a+1]
   T h2src = T(0);           // E_t[a+1][a-1] (lane a-1's E_t[(a-1)+2][a-1])
   T dx_out = T(0), dy_out = T(0);
-  Q2* rq = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  T* rq = rec + (size_t)pair * (kCrossMaxInner * W) * W;
   T rt = T(0);  // tangent of the latest solved rotation; its fp64 record is
                 // written at the start of the next phase (steps 0 .. gs-1 are
                 // recorded; the look-ahead rotation solved in the final phase
@@ -1319,16 +1324,9 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     smax = fmaxf(smax, eff_sine(rs, rdx, rdy));
     rcount += rs != T(0) ? 1u : 0u;
     if constexpr ((ABL & 1) != 0) return;
-    double c64, s64;
-    if constexpr (sizeof(T) == 8) {
-      c64 = rc;
-      s64 = rs;
-    } else {  // fp64 (c, s) of the fp32 t, normalised in fp64 (Q stays orthogonal)
-      const double td = (double)rt;
-      c64 = rsqrt64(fma(td, td, 1.0));
-      s64 = td * c64;
-    }
-    if (step < kCrossMaxInner * W) rq[(size_t)step * W + a] = Q2{c64, s64};
+    // the tangent only: the Q builds form the fp64 (c, s) from it
+    // (rotation_cs), off this lane's step
+    if (step < kCrossMaxInner * W) rq[(size_t)step * W + a] = rt;
   };
   int racc = 0, racc_next = 0;
   if (run && solver) {  // step 0 of slot a
@@ -1400,7 +1398,11 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
           Eb[nb][wr1[j]] = cc * e1[j] - ss * e0[j];
         }
     }
-    __syncthreads();
+    // LDS-only barrier: __syncthreads would also wait for the record stores
+    // (vmcnt(0)) every step; nothing in the loop reads global memory
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     ++gs;
     if (++st < W) return false;
     st = 0;
@@ -1446,13 +1448,24 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
 // records once for 4x the rows).
 constexpr int kQbThreads = 256;
 constexpr int kQbChunk = 64;  // steps staged in LDS at a time
+// fp64 (c, s) of a recorded tangent (evd_cross_kernel records t only):
+// fp32 data -- the fp32 t normalised in fp64 (Q stays orthogonal to fp64
+// rounding); fp64 data -- rotation_fast's own c = 1 / sqrt(1 + t^2), s = t c.
+__device__ __forceinline__ Pair2<double> rotation_cs(float t) {
+  const double td = (double)t, c = rsqrt64(fma(td, td, 1.0));
+  return Pair2<double>{c, td * c};
+}
+__device__ __forceinline__ Pair2<double> rotation_cs(double t) {
+  const double c = 1.0 / sqrt(fma(t, t, 1.0));
+  return Pair2<double>{c, t * c};
+}
 template <int W, int R>
 __host__ __device__ constexpr int qbuild_blocks() {  // workgroups per pair
   return (2 * W) / (R * (SVDJ_WAVE / W) * (kQbThreads / SVDJ_WAVE));
 }
 template <typename T, int W, int R>
 __global__ __launch_bounds__(kQbThreads) void qbuild_kernel(
-    const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
+    const T* __restrict__ rec, const int32_t* __restrict__ nsteps,
     const int32_t* __restrict__ skip, T* __restrict__ Qall) {
   constexpr int N = 2 * W;
   constexpr int GPW = SVDJ_WAVE / W;
@@ -1465,7 +1478,7 @@ __global__ __launch_bounds__(kQbThreads) void qbuild_kernel(
   const int a = lane % W;
   const int k0 = ((blockIdx.y * (kQbThreads / SVDJ_WAVE) + wave) * GPW + lane / W) * R;
   const int ns = nsteps[pair];
-  const Q2* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  const T* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
   double qx[R], qy[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
@@ -1474,7 +1487,7 @@ __global__ __launch_bounds__(kQbThreads) void qbuild_kernel(
   }
   for (int t0 = 0; t0 < ns; t0 += kQbChunk) {
     const int nc = ns - t0 < kQbChunk ? ns - t0 : kQbChunk;
-    for (int i = threadIdx.x; i < nc * W; i += kQbThreads) rs[i] = rp[(size_t)t0 * W + i];
+    for (int i = threadIdx.x; i < nc * W; i += kQbThreads) rs[i] = rotation_cs(rp[(size_t)t0 * W + i]);
     __syncthreads();
     Q2 n0 = rs[a], n1 = nc > 1 ? rs[W + a] : Q2{1.0, 0.0};
     for (int t = 0; t < nc; ++t) {
@@ -1932,7 +1945,7 @@ __host__ __device__ constexpr size_t ts_frag(int q, int kb, int ct, int cs, int 
 // fragment (k block k0 / 32, lane group (k0 / 8) & 3).
 template <int PHASE, int R, int NT, int NP = 0>
 __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
-    const Pair2<double>* __restrict__ rec, const int32_t* __restrict__ nsteps,
+    const float* __restrict__ rec, const int32_t* __restrict__ nsteps,
     const int32_t* __restrict__ skip, double* __restrict__ T1, bf16x8* __restrict__ Ts = nullptr) {
   static_assert(PHASE == 1 ? NP == 0 : ((NP == 2 || NP == 3) && (R == 2 || R == 4 || R == 8)),
                 "phase 2: split T - I, 2 / 4 / 8 rows per thread");
@@ -1946,7 +1959,7 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
   const int a = lane;
   const int k0 = (blockIdx.y * WAVES + wave) * R;
   const int ns = skip[pair] ? 0 : nsteps[pair];
-  const Q2* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
+  const float* rp = rec + (size_t)pair * (kCrossMaxInner * W) * W;
   const int q = pair >> 1, j = pair & 1;
   double qx[R], qy[R];
   if constexpr (PHASE == 1) {
@@ -1971,7 +1984,7 @@ __global__ __launch_bounds__(NT) void qbuild_quad_kernel(
   }
   for (int t0 = 0; t0 < ns; t0 += kQbChunk) {
     const int nc = ns - t0 < kQbChunk ? ns - t0 : kQbChunk;
-    for (int i = threadIdx.x; i < nc * W; i += NT) rs[i] = rp[(size_t)t0 * W + i];
+    for (int i = threadIdx.x; i < nc * W; i += NT) rs[i] = rotation_cs(rp[(size_t)t0 * W + i]);
     __syncthreads();
     Q2 n0 = rs[a], n1 = nc > 1 ? rs[W + a] : Q2{1.0, 0.0};
     for (int t = 0; t < nc; ++t) {
@@ -2746,7 +2759,7 @@ static size_t ws_bytes_for(int esize, int W, int P, int m_pad, bool quad) {
   size_t slabs = (size_t)P * g.gchunks * 4 * W * W * esize;
   size_t q = (size_t)P * 4 * W * W * esize;
   size_t sk = (size_t)P * sizeof(int32_t);
-  size_t rec = (size_t)P * kCrossMaxInner * W * W * sizeof(Pair2<double>);
+  size_t rec = (size_t)P * kCrossMaxInner * W * W * esize;
   // slabs + double-buffered Q and skip flags (evd(s+1) may run while apply(s)
   // reads) + the cross EVD's rotation records and step counts (consumed by
   // qbuild(s) before evd(s+1) on the same stream: single-buffered)
@@ -2765,7 +2778,7 @@ struct Chain {
   T* slabs;
   T* Qb[2];
   int32_t* skipb[2];
-  Pair2<double>* rec;  // cross EVD rotation records
+  T* rec;  // cross EVD rotation records (tangents)
   int32_t* nsteps;
   // quad steps (has_quad)
   float* qslabs;
@@ -2814,8 +2827,8 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   c.skipb[0] = (int32_t*)w;
   c.skipb[1] = (int32_t*)(w + kstride);
   w += 2 * kstride;
-  c.rec = (Pair2<double>*)w;
-  w += rup256((size_t)P * kCrossMaxInner * W * W * sizeof(Pair2<double>));
+  c.rec = (T*)w;
+  w += rup256((size_t)P * kCrossMaxInner * W * W * sizeof(T));
   c.nsteps = (int32_t*)w;
   w += kstride;
   c.qslabs = nullptr;

@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
   int32_t *dp, *dsk, *dns;
   float *dsl, *dD, *dQ;
   uint32_t* dm;
-  svdj::Pair2<double>* drec;
+  float* drec;
   (void)hipMalloc(&drec, (size_t)P * svdj::kCrossMaxInner * W * W * sizeof(*drec));
   (void)hipMalloc(&dns, P * 4);
   (void)hipMalloc(&dp, hp.size() * 4);
