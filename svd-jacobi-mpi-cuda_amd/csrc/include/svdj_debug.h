@@ -5,8 +5,6 @@
 //     merge=0|1            one-GPU merged issue of the two chains forced off/on
 //                          (world 1 only, both engines: svdj_dist_issue_rules,
 //                          parallel/distributed.py choose_merged)
-//     merge_dist=1         Python engine, P > 1: the merged issue with exchanges
-//                          (PipelineExecutor.run(merge=True))
 //     gram_chunks=N        row chunks of the single-step Gram (make_geometry)
 //     quad_gram_chunks=N   row chunks of the quad Gram (quad_geometry)
 //     stream_order=B       row-chunk dispatch order: bit 0 cross Gram chunks

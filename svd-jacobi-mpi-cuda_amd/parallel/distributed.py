@@ -339,11 +339,11 @@ class DistributedBlockJacobi(Solver):
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
         # 39.4 -> 36.9 ms, profiles/r5_quad2), and so do quad steps of 16
         # pairs (4096^2 135.4 -> 123.5 ms, profiles/r6_issue).  SVDJ_DEBUG merge=0/1
-        # overrides; with exchanges merging was slower at every P (SVDJ_DEBUG
-        # merge_dist=1 selects it there, A/B only, this engine only).
-        merged = pipelined and dev.type == "cuda" and (
-            choose_merged(P if comm.distributed else 1, k, quad)
-            or (comm.distributed and debug_knob("merge_dist") == 1))
+        # overrides; with exchanges merging was slower at every P (round 6,
+        # 16384^2 P = 8: 51.9 ms per sweep merged, 50.6 merged with quad
+        # steps, 43.1 not merged; profiles/r6_issue/plan_p8).
+        merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
+                                                                    k, quad)
         for sw in range(start, cfg.max_sweeps):
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
