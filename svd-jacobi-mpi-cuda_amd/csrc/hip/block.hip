@@ -1168,25 +1168,32 @@ __global__ __launch_bounds__(evd_threads(W)) void evd_kernel(
 // pairs, W = 64): register Q accumulation and the solve chain made the
 // per-step time ~2000 cycles; the G update itself was not the limit.  Round
 // 6 ablations (profiles/r6_evd): of 33 us per launch, 14 us are barriers,
-// lane rotates and bookkeeping; the fp64 (c, s) of each record cost 3.8 us
-// on the solver lane (now formed by the Q builds), the rotation solve 6 us.
-template <int W>
-__host__ __device__ constexpr int cross_threads() { return W == 64 ? 1024 : 512; }
+// lane rotates, bookkeeping, assembly and launch; the records cost 3.8 us
+// (their fp64 (c, s), now formed by the Q builds, and the per-step wait for
+// their stores), the rotation solve 6 us.
+// DPW: coupling diagonals per wave >= 1 (W = 64; W = 32 keeps 2, one per lane half)
+template <int W, int DPW = 2>
+__host__ __device__ constexpr int cross_threads() {
+  return W == 64 ? SVDJ_WAVE * (1 + (W / 2 - 2 + DPW - 1) / DPW) : 512;
+}
 constexpr int kCrossMaxInner = 4;  // inner sweeps whose rotation records fit the workspace
 
 // ABL (tools/micro/evd_bench.hip only; production launches ABL = 0): bit 0
 // no rotation records; bit 1 waves >= 1 skip their coupling updates
 // (barriers kept); bit 2 the solver lane skips the rotation (c = 1, s = 0);
-// bit 3 the solver lane skips its LDS coupling read and write.
-template <typename T, int W, int ABL = 0>
-__global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
+// bit 3 the solver lane skips its LDS coupling read and write; bit 4 no
+// steps at all (assembly, launch and the epilogue only).
+template <typename T, int W, int ABL = 0, int DPW = 2>
+__global__ __launch_bounds__((cross_threads<W, DPW>())) void evd_cross_kernel(
     const int32_t* __restrict__ pairs, const T* __restrict__ slabs, int nchunk,
     T* __restrict__ D, T* __restrict__ rec, int32_t* __restrict__ nsteps,
     int32_t* __restrict__ skip, T tol, int absmode, int max_inner, uint32_t* __restrict__ metric) {
   static_assert(W == 32 || W == 64, "cross EVD: W = 32 or 64");
-  constexpr int NT = cross_threads<W>();
+  static_assert(W == 64 || DPW == 2, "W = 32: two diagonals per wave (one per lane half)");
+  constexpr int NT = cross_threads<W, DPW>();
   constexpr int NWAVE = NT / SVDJ_WAVE;
-  static_assert(NWAVE - 1 == (W / 2 - 2) / 2, "two diagonals per wave >= 1");
+  static_assert(W == 32 ? NWAVE - 1 == (W / 2 - 2) / 2 : NWAVE - 1 == (W / 2 - 2 + DPW - 1) / DPW,
+                "DPW diagonals per wave >= 1");
   constexpr int N = 2 * W;
   using T2 = Pair2<T>;
   using Q2 = Pair2<double>;
@@ -1257,31 +1264,28 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
     }
     __syncthreads();
   }
-  const bool run = need_any != 0;
+  const bool run = need_any != 0 && (ABL & 16) == 0;
   const int inner = max_inner < kCrossMaxInner ? max_inner : kCrossMaxInner;
 
-  // ---- LDS groups of waves >= 1: (i, d), d = 2w+1, 2w+2 (W = 64: both on
-  // every lane; W = 32: lanes 0..31 the first, 32..63 the second)
-  int gi[2] = {0, 0}, gp[2] = {0, 0}, rd0[2], rd1[2], wr0[2], wr1[2];
-  int ng = 0;
-  auto add_group = [&](int i, int d) {
-    if (d == W / 2 && i >= W / 2) return;  // the half diagonal has W/2 groups
+  // ---- LDS groups of waves >= 1: (i, d), d = DPW (w - 1) + 3 + j (W = 64:
+  // all on every lane; W = 32: d = 2w+1 on lanes 0..31, 2w+2 on 32..63);
+  // gv bit j: group j exists on this lane (the half diagonal has W/2 groups)
+  constexpr int G = W == 64 ? DPW : 1;
+  int gi[G], gp[G], rd0[G], rd1[G], wr0[G], wr1[G];
+  uint32_t gv = 0;
+#pragma unroll
+  for (int jg = 0; jg < G; ++jg) {
+    const int i = W == 64 ? lane : (lane & 31);
+    const int d = W == 64 ? DPW * (wave - 1) + 3 + jg : 2 * wave + 1 + (lane >> 5);
+    const bool ok = wave >= 1 && d <= W / 2 && !(d == W / 2 && i >= W / 2);
     const int p = (i + d) % W;
-    gi[ng] = i;
-    gp[ng] = p;
-    rd0[ng] = i * W + p;
-    rd1[ng] = p * W + i;
-    wr0[ng] = i * W + (p + W - 1) % W;
-    wr1[ng] = p * W + (i + W - 1) % W;
-    ++ng;
-  };
-  if (wave >= 1) {
-    if constexpr (W == 64) {
-      add_group(lane, 2 * wave + 1);
-      add_group(lane, 2 * wave + 2);
-    } else {
-      add_group(lane & 31, 2 * wave + 1 + (lane >> 5));
-    }
+    gi[jg] = i;
+    gp[jg] = p;
+    rd0[jg] = i * W + p;
+    rd1[jg] = p * W + i;
+    wr0[jg] = i * W + (p + W - 1) % W;
+    wr1[jg] = p * W + (i + W - 1) % W;
+    gv |= ok ? 1u << jg : 0u;
   }
 
   // ---- solver lanes (wave 0, lane a < W): slot a's state in registers
@@ -1380,19 +1384,19 @@ __global__ __launch_bounds__(cross_threads<W>()) void evd_cross_kernel(
         racc_next = 0;
       }
     } else if constexpr ((ABL & 2) == 0) {
-      T e0[2], e1[2];
-      T2 ri[2], rp[2];
+      T e0[G], e1[G];
+      T2 ri[G], rp[G];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < ng) {
+      for (int j = 0; j < G; ++j)
+        if (gv >> j & 1u) {
           e0[j] = Eb[b][rd0[j]];
           e1[j] = Eb[b][rd1[j]];
           ri[j] = rcs[b][gi[j]];
           rp[j] = rcs[b][gp[j]];
         }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < ng) {
+      for (int j = 0; j < G; ++j)
+        if (gv >> j & 1u) {
           const T cc = ri[j].x * rp[j].x, ss = ri[j].y * rp[j].y;
           Eb[nb][wr0[j]] = cc * e0[j] - ss * e1[j];
           Eb[nb][wr1[j]] = cc * e1[j] - ss * e0[j];

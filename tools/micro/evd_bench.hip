@@ -95,6 +95,27 @@ int main(int argc, char** argv) {
   abl(std::integral_constant<int, 3>{}, "records off, waves >= 1 idle");
   abl(std::integral_constant<int, 7>{}, "records off, idle, no solve");
   abl(std::integral_constant<int, 15>{}, "all off (barriers, DPP, bookkeeping)");
+  abl(std::integral_constant<int, 16>{}, "no steps (assembly, launch, epilogue)");
+  // diagonals per wave >= 1 (fewer waves at each step's barrier, more LDS work per wave)
+  auto dpw = [&](auto dc) {
+    constexpr int D = decltype(dc)::value;
+    reset();
+    const double t = time_it([&]() {
+      hipLaunchKernelGGL((svdj::evd_cross_kernel<float, W, 0, D>), dim3(P),
+                         dim3(svdj::cross_threads<W, D>()), 0, nullptr, dp, dsl, nchunk, dD, drec,
+                         dns, dsk, 1e-6f, 0, 1, dm);
+    }, reps);
+    std::printf("  dpw %2d (%4d threads)                           %.2f us\n", D,
+                svdj::cross_threads<W, D>(), t);
+  };
+  dpw(std::integral_constant<int, 2>{});
+  dpw(std::integral_constant<int, 3>{});
+  dpw(std::integral_constant<int, 4>{});
+  dpw(std::integral_constant<int, 5>{});
+  dpw(std::integral_constant<int, 6>{});
+  dpw(std::integral_constant<int, 8>{});
+  dpw(std::integral_constant<int, 10>{});
+  dpw(std::integral_constant<int, 15>{});
 #endif
   return 0;
 }
