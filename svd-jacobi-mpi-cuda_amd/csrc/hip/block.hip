@@ -2168,8 +2168,8 @@ __global__ __launch_bounds__(NT) void quad_update_kernel(
 // extra lane offsets took from the T slice.)
 // Work: the active quads (some step-s or step-(s+1) pair rotated) are listed
 // by every wave with ballots over the skip flags (no extra launch, no host
-// sync); nact active quads x S row slices, S = max(1, grid / nact), are dealt
-// to the persistent grid (one workgroup per CU: the LDS is 160 KB).
+// sync); their tiles, flattened, are dealt to the persistent grid in equal
+// contiguous ranges (one workgroup per CU: the LDS is 160 KB).
 constexpr int kQuadTsThreads = 512;
 constexpr int kQuadTsGrid = 256;
 template <int NP>
@@ -2216,12 +2216,19 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
   int nact = 0;
   for (int b0 = 0; b0 < nq; b0 += SVDJ_WAVE) nact += __popcll(__ballot(active(b0 + lane)));
   if (nact == 0) return;
-  const int G = (int)gridDim.x;
-  const int S = G / nact > 1 ? G / nact : 1;
-  const int nitems = nact * S, nt = a_tiles + v_tiles;
-
-  for (int item = blockIdx.x; item < nitems; item += G) {
-    const int qi = item / S, sl = item % S;
+  const int G = (int)gridDim.x, nt = a_tiles + v_tiles;
+  // The active quads' tiles, flattened quad-major, are dealt to the grid in
+  // equal contiguous ranges (a range may span two quads: one more T-slice
+  // load).  Round 5 split each quad into G / nact equal slices, which left
+  // G mod nact workgroups idle -- up to a quarter of the grid (52 active
+  // quads: 208 of 256 busy) once quads start to skip.
+  const long long total = (long long)nact * nt;
+  const long long g_end = (long long)(blockIdx.x + 1) * total / G;
+  for (long long pos = (long long)blockIdx.x * total / G; pos < g_end;) {
+    const int qi = (int)(pos / nt);
+    const int t0 = (int)(pos % nt);
+    const int t1 = (int)((long long)t0 + (g_end - pos) < nt ? (long long)t0 + (g_end - pos) : nt);
+    pos += t1 - t0;
     int q = 0;
     for (int b0 = 0, seen = 0; b0 < nq; b0 += SVDJ_WAVE) {  // the qi-th active quad
       const bool a = active(b0 + lane);
@@ -2234,7 +2241,6 @@ apply_quad_ts_kernel(float* __restrict__ A, int lda, int a_tiles, float* __restr
       seen += cnt;
     }
     q = __builtin_amdgcn_readfirstlane(q);
-    const int t0 = (int)((long long)sl * nt / S), t1 = (int)((long long)(sl + 1) * nt / S);
     // this wave's split T - I slice: Ts[q][kb][ct = wave][cs][part][lane]
     bf16x8 qf[8][2][NP];
 #pragma unroll
