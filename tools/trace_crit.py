@@ -51,8 +51,8 @@ def kind(name):
     n = name.lower()
     if "svdj" not in n:
         return "torch"   # copies (simulated exchanges, copy-in), generator, norms
-    if "qbuild" in n:  # the cross EVD's Q build: part of the EVD phase
-        return "evd"
+    if any(k in n for k in ("qbuild", "quad_update", "slab_reduce")):
+        return "evd"  # the latency chain of a (quad) step: Q builds, Gram-space update
     for k in ("gram", "evd", "apply"):
         if k in n:
             return k
