@@ -2993,9 +2993,24 @@ static int launch_gram_evd(const Chain<T>& c, int s, double tol, int absmode, in
   }
   SVDJ_LAUNCH_CHECK();
   if (mode == 3) {
+    // many row chunks (few pairs per step: the 8-GPU plans read 32): sum them
+    // once, wide, instead of on the EVD's critical path (one workgroup per
+    // pair reading every chunk); bitwise the same sums (slab_reduce_kernel)
+    const T* gs = c.slabs;
+    int gn = c.g.gchunks;
+    if constexpr (sizeof(T) == 4 && W == 64) {
+      static const int red_from = svdj_debug_knob("cross_reduce_chunks", 9);  // A/B only
+      if (gn >= red_from) {
+        float* red = c.slabs + (size_t)c.P * gn * W * W;  // inside the full-Gram slab area
+        hipLaunchKernelGGL(slab_reduce_kernel, dim3(c.P, W * W / 4 / kRedThreads), dim3(kRedThreads),
+                           0, c.st, c.slabs, gn, red);
+        SVDJ_LAUNCH_CHECK();
+        gs = red;
+        gn = 1;
+      }
+    }
     hipLaunchKernelGGL((evd_cross_kernel<T, W>), dim3(c.P), dim3(cross_threads<W>()), 0, c.st, pr,
-                       c.slabs, c.g.gchunks, c.D, c.rec, c.nsteps, c.skipb[b], (T)tol, absmode,
-                       max_inner, metric);
+                       gs, gn, c.D, c.rec, c.nsteps, c.skipb[b], (T)tol, absmode, max_inner, metric);
     SVDJ_LAUNCH_CHECK();
     constexpr int RL = W == 64 ? 16 : 8;  // one workgroup per pair
     // 16 rows per lane from 64 pairs per step; at 32 pairs 4 rows per lane is

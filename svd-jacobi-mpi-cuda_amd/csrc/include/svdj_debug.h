@@ -13,6 +13,8 @@
 //                          |T - I| <= 2^-K (default 7)
 //     qb1_threads=N        phase-1 quad Q build workgroup size (1024 or 512)
 //     upd_threads=N        quad_update_kernel workgroup size (256 or 512)
+//     cross_reduce_chunks=N  single cross steps (fp32 W = 64): pre-sum the Gram's
+//                          row chunks when there are at least N (default 9)
 //
 // svdj_debug_knob returns the value of `key`, or `dflt` when SVDJ_DEBUG is
 // unset or does not name it.  Host code only; callers cache the result.
