@@ -2505,13 +2505,28 @@ static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
 // Partners of column tile w (tile t is block t >> 1 of [a b c d], half t & 1):
 // the 24 pairs of tiles from different blocks, each listed once, 3 per tile
 // (3 bits each, partner j at bits 3j).
+constexpr int kGramPartners[8] = {2 | 3 << 3 | 4 << 6, 2 | 3 << 3 | 5 << 6, 4 | 5 << 3 | 6 << 6,
+                                  4 | 5 << 3 | 7 << 6, 1 | 6 << 3 | 7 << 6, 0 | 6 << 3 | 7 << 6,
+                                  0 | 1 << 3 | 3 << 6, 0 | 1 << 3 | 2 << 6};
+// every unordered pair of tiles from different blocks exactly once, none within a block
+constexpr bool gram_partners_cover() {
+  int seen[8][8] = {};
+  for (int w = 0; w < 8; ++w)
+    for (int j = 0; j < 3; ++j) {
+      const int y = kGramPartners[w] >> (3 * j) & 7;
+      if ((y >> 1) == (w >> 1)) return false;
+      ++seen[w < y ? w : y][w < y ? y : w];
+    }
+  for (int x = 0; x < 8; ++x)
+    for (int y = x + 1; y < 8; ++y)
+      if (seen[x][y] != ((x >> 1) != (y >> 1) ? 1 : 0)) return false;
+  return true;
+}
+static_assert(gram_partners_cover(), "quad Gram partner table");
 __device__ __forceinline__ int gram_partners(int w) {
-  constexpr int PK[8] = {2 | 3 << 3 | 4 << 6, 2 | 3 << 3 | 5 << 6, 4 | 5 << 3 | 6 << 6,
-                         4 | 5 << 3 | 7 << 6, 1 | 6 << 3 | 7 << 6, 0 | 6 << 3 | 7 << 6,
-                         0 | 1 << 3 | 3 << 6, 0 | 1 << 3 | 2 << 6};
-  int r = PK[0];
+  int r = kGramPartners[0];
 #pragma unroll
-  for (int t = 1; t < 8; ++t) r = w == t ? PK[t] : r;
+  for (int t = 1; t < 8; ++t) r = w == t ? kGramPartners[t] : r;
   return r;
 }
 // Product (slab) of blocks (x, y) of [a b c d]: ac bd ad bc ab cd = 0 .. 5;
