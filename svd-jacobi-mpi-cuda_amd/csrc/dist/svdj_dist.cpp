@@ -1107,6 +1107,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   std::vector<std::pair<double, double>> busy, waits;
   double comm_ms = 0, sweep_base_ms = 0;
   long long n_exch = 0, n_bytes = 0;
+  int mma_sweep = p->mma;  // the apply's mode, | 256 for a 2-part quad Gram (below)
   // One sweep: every dependency is an event; the host never waits.
   auto sweep = [&]() -> int {
     std::vector<hipEvent_t> last[4];   // task events on each half since its last exchange
@@ -1119,7 +1120,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
                                h->merged_pairs + h->merged_off[m], h->merged_np[m],
                                h->merged_steps[m], h->merged_modes[m].data(), p->tol, p->tol_mode,
-                               1, h->ws[0], h->wsb, h->metric, p->mma, sa));
+                               1, h->ws[0], h->wsb, h->metric, mma_sweep, sa));
       return 0;
     }
     if (h->timing) HIPC(hipEventRecord(h->ev_t0, sa));
@@ -1198,7 +1199,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         const int cz = z.stream;
         SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
                                dev_pairs(z), z.t->npairs, z.t->steps, z.t->modes.data(), p->tol,
-                               p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, p->mma, st[cz]));
+                               p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, mma_sweep, st[cz]));
       }
       for (int q = 0; q < n_t; ++q) {
         const Item& x = items[idx[q]];
@@ -1251,7 +1252,14 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
   p->calib_direct_ms = h->calib_ms[0];
   p->calib_spread_ms = h->calib_ms[1];
   const auto t_solve = std::chrono::steady_clock::now();
+  // Quad Gram precision per sweep (parallel/distributed.py, the same rule):
+  // 2 bf16 parts (svdj_block_steps' mma bit 8) while the previous sweep
+  // rotated every pair; SVDJ_DEBUG gram2=0/1 forces it off / on (A/B).
+  const long long nbt = 2LL * P * h->k, all_pairs = nbt * (nbt - 1) / 2;
+  const int gram2 = svdj_debug_knob("gram2", -1);
+  bool prev_all = true;
   for (int sw = 0; sw < p->max_sweeps && !rc; ++sw) {
+    mma_sweep = p->mma | ((h->quad && (gram2 < 0 ? prev_all : gram2 == 1)) ? 256 : 0);
     if ((rc = sweep())) break;
     // ---- stop test (svdj_stop.h): global max convergence value and largest
     // applied |sin| (positive floats order as uint32), total rotated pairs
@@ -1279,6 +1287,7 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
     float mx, ms;
     memcpy(&mx, &hm[0], sizeof(float));
     memcpy(&ms, &hm[4], sizeof(float));
+    prev_all = (long long)hm[1] >= all_pairs;
     if (p->hist) p->hist[sw] = mx;
     p->sweeps = sw + 1;
     if (p->progress && g == 0) {

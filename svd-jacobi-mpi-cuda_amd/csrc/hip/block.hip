@@ -2496,12 +2496,13 @@ __global__ __launch_bounds__(kRedThreads) void slab_reduce_kernel(const float* _
 //     (the order quad_update_kernel reads), one W x W slab per row chunk; a
 //     tile whose owner is its slab's column block is stored transposed.
 constexpr int kGramQThreads = 512;
+template <int NP>
 struct GramQLds {
-  static constexpr int S_BYTES = 8 * 2 * 3 * SVDJ_WAVE * 16;  // 8 col tiles x 2 sub-tiles x 3 parts
-  static constexpr int R_BYTES = 8 * 32 * 32 * 4;             // raw 32-row slab, wave w at 4 KB * w
+  static constexpr int S_BYTES = 8 * 2 * NP * SVDJ_WAVE * 16;  // 8 col tiles x 2 sub-tiles x NP parts
+  static constexpr int R_BYTES = 8 * 32 * 32 * 4;              // raw 32-row slab, wave w at 4 KB * w
   static constexpr int TOTAL = 2 * S_BYTES + 2 * R_BYTES;
 };
-static_assert(GramQLds::TOTAL <= 163840, "quad Gram LDS");
+static_assert(GramQLds<3>::TOTAL <= 163840, "quad Gram LDS");
 // Partners of column tile w (tile t is block t >> 1 of [a b c d], half t & 1):
 // the 24 pairs of tiles from different blocks, each listed once, 3 per tile
 // (3 bits each, partner j at bits 3j).
@@ -2542,12 +2543,15 @@ static_assert(gram_product(2, 0) == 8 && gram_product(3, 2) == 13, "gram_product
 // ABL (tools/micro/quad_apply_ab.hip only; production launches ABL = 0):
 // bit 0 one MFMA per output sub-tile and slab instead of 6; bit 1 no global
 // reads (no DMA, no waits).
-template <int ABL = 0>
+// NP = 2 (sweeps far from convergence, see launch_quad_gram_evd): 2 bf16
+// parts and the 3 products of order < 2 -- couplings to ~2^-17 |x||y|,
+// which only steers the rotation angles (T stays orthogonal to fp64).
+template <int ABL = 0, int NP = 3>
 __global__ __launch_bounds__(kGramQThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t* __restrict__ pairs,
                  int P, int rows_per_chunk, float* __restrict__ slabs) {
-  constexpr int W = 64, NP = 3;
-  using L = GramQLds;
+  constexpr int W = 64;
+  using L = GramQLds<NP>;
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   const int q = blockIdx.x, chunk = blockIdx.y, nchunk = gridDim.y;
   const int lane = threadIdx.x & 63;
@@ -2619,8 +2623,9 @@ gram_quad_kernel(const float* __restrict__ A, int lda, int m_pad, const int32_t*
         for (int s = 0; s < 2; ++s) {
           if constexpr ((ABL & 1) != 0) {
             using i32x4 = __attribute__((ext_vector_type(4))) int;
-            i32x4 yy = __builtin_bit_cast(i32x4, yf[0]) ^ __builtin_bit_cast(i32x4, yf[1]) ^
-                       __builtin_bit_cast(i32x4, yf[2]);
+            i32x4 yy = __builtin_bit_cast(i32x4, yf[0]);
+#pragma unroll
+            for (int i = 1; i < NP; ++i) yy ^= __builtin_bit_cast(i32x4, yf[i]);
             acc[j][s][s2] = mfma16(xf[s][0], __builtin_bit_cast(bf16x8, yy), acc[j][s][s2]);
           } else {
 #pragma unroll
@@ -2814,6 +2819,7 @@ struct Chain {
   int32_t* skip1[2];
   int32_t* skip2[2];
   hipStream_t st;
+  int gram_np;  // bf16 parts of the quad Gram (3; 2 far from convergence)
 };
 
 template <typename T, int W>
@@ -2839,6 +2845,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
     return -2;
   }
   c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
+  c.gram_np = 3;
   c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
   c.g = make_geometry(W, P, m_pad, V ? n_v : 0, mma);
   char* w = (char*)ws;
@@ -2896,8 +2903,12 @@ static int launch_quad_gram_evd(const Chain<T>& c, int s, double tol, int absmod
     const int b = s & 1;
     const int32_t* pr = c.pairs + (size_t)s * c.P * 2;
     const int32_t* pr1 = pr + 2 * c.P;
-    hipLaunchKernelGGL(gram_quad_kernel<0>, dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0, c.st,
-                       c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
+    if (c.gram_np == 2)
+      hipLaunchKernelGGL((gram_quad_kernel<0, 2>), dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0,
+                         c.st, c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
+    else
+      hipLaunchKernelGGL((gram_quad_kernel<0, 3>), dim3(c.P / 2, c.g.qgch), dim3(kGramQThreads), 0,
+                         c.st, c.A, c.lda, c.m_pad, pr, c.P, c.g.qgrows, c.qslabs);
     SVDJ_LAUNCH_CHECK();
     // many row chunks (few quads): sum them once, wide, for both consumers
     const bool red = c.g.qgch > 4;
@@ -3180,9 +3191,12 @@ static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv
                           double tol, int absmode, int max_inner, void* ws, size_t ws_bytes,
                           uint32_t* metric, int mma, void* stream) {
   Chain<T> c;
+  const int gram2 = (mma >> 8) & 1;  // svdj_block_steps' mma bit 8
+  mma &= 0xff;
   int rc = chain_init<T, W>(c, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
                             ws, ws_bytes, mma, (hipStream_t)stream);
   if (rc) return rc;
+  if (gram2) c.gram_np = 2;
   return block_steps_t<T, W>(c, tol, absmode, max_inner, metric, mma);
 }
 
@@ -3191,7 +3205,9 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
                                 const int32_t* modes, double tol, int tol_mode, int max_inner,
                                 void* ws, size_t ws_bytes, uint32_t* metric, int mma,
                                 void* stream) {
-  int rc = check_dims(m_pad, lda, V, n_v, ldv, mma);
+  // mma bits 0-7: the apply's matrix-core mode; bit 8: quad Gram with 2 bf16
+  // parts (gram_quad_kernel<0, 2>) for sweeps far from convergence
+  int rc = check_dims(m_pad, lda, V, n_v, ldv, mma & 0xff);
   if (rc) return rc;
   if (tol_mode != 0 && tol_mode != 1) {
     set_error("bad tol_mode %d (0 relative, 1 absolute)", tol_mode);

@@ -15,6 +15,9 @@
 //     upd_threads=N        quad_update_kernel workgroup size (256 or 512)
 //     cross_reduce_chunks=N  single cross steps (fp32 W = 64): pre-sum the Gram's
 //                          row chunks when there are at least N (default 9)
+//     gram2=0|1            quad Gram on 2 bf16 parts forced off / on (default:
+//                          while the previous sweep rotated every pair; both
+//                          engines: parallel/distributed.py, svdj_dist_solve)
 //
 // svdj_debug_knob returns the value of `key`, or `dflt` when SVDJ_DEBUG is
 // unset or does not name it.  Host code only; callers cache the result.

@@ -72,6 +72,9 @@ int svdj_scalar_solve(int dtype, int m_pad, void* A, int lda, void* V, int n_v,
 //           MFMA with a 3-way bf16 split (6 products, fp32-level accuracy),
 //           2 fp32 data on bf16 MFMA with a 2-way split (3 products, ~2^-17).
 //           Both split modes apply Y = X + X (Q - I), the identity in fp32.
+//           Bit 8 (| 256): the quad Gram of quad steps with 2 bf16 parts (3
+//           products, couplings to ~2^-17) -- for sweeps far from convergence,
+//           where it only steers the rotation angles.
 // Workspace size for steps of P pairs: svdj_block_workspace_bytes(); quad != 0
 // when the step list holds quad steps (modes 4/5: fp32, W = 64).
 size_t svdj_block_workspace_bytes(int dtype, int W, int P, int m_pad, int quad);

@@ -329,7 +329,7 @@ class DistributedBlockJacobi(Solver):
                 work["gram_quads"] += sum(1 for x in modes if int(x) == 4) * (pairs.shape[1] // 2)
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                              inner_order=inner)
+                              inner_order=inner, gram_parts=gram_parts[0])
         # One rank, no exchanges, >= 64 pairs per chain step (>= 32 with quad
         # steps): the two chains' parallel tasks merged into single launches
         # of twice the pairs (PipelineExecutor.run_merged), the EVD latency
@@ -344,7 +344,20 @@ class DistributedBlockJacobi(Solver):
         # steps, 43.1 not merged; profiles/r6_issue/plan_p8).
         merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
                                                                     k, quad)
+        # Quad Gram precision per sweep: while the previous sweep rotated
+        # every pair (far from convergence: the first ~12 of 18 sweeps at
+        # 16384^2), the couplings only steer rotation angles and the 2-part
+        # Gram (2^-17) does; later sweeps need the exact one.  SVDJ_DEBUG
+        # gram2=0/1 forces it off / on (A/B).
+        nbt = 2 * P * k
+        all_pairs = nbt * (nbt - 1) // 2
+        # (libsvdj_dist: the same rule in svdj_dist_solve)
+        gram2 = debug_knob("gram2")
+        gram_parts = [3]
+        prev_all = start == 0
         for sw in range(start, cfg.max_sweeps):
+            use2 = prev_all if gram2 is None else gram2 == 1
+            gram_parts[0] = 2 if (quad and use2) else 3
             with trace_range(f"svdj.sweep{sw}"):
                 K.reset_metric(metric)
                 if pipelined and merged and not comm.distributed:
@@ -364,6 +377,7 @@ class DistributedBlockJacobi(Solver):
                                       cfg.max_inner_sweeps, metric, mma=mma, pool=self._ws,
                                       tol_mode=cfg.tol_mode, inner_order=inner)
                 mx, ms, nrot, ncr = self._reduce_metric(metric, dev)
+                prev_all = int(nrot) >= all_pairs
                 work_acc += K.metric_work(metric)
             hist.append(mx)
             sweeps = sw + 1
