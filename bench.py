@@ -527,15 +527,16 @@ def work_estimate(counts, m_pad, seconds):
     """Executed matrix-core work and HBM traffic of the quad kernels per
     solve, next to the algorithmic GFLOP/s (the headline is the
     reference's scalar-Jacobi flop count, which is not what the MFMAs
-    execute).  counts = [apply MFMAs, apply tiles, quad Grams] summed over
-    ranks: one v_mfma_f32_32x32x16_bf16 = 32768 flops; an apply tile is 32
-    rows x 256 columns of A or V read and written (64 KiB); a quad Gram reads
-    256 columns of m_pad rows and issues 288 MFMAs per 32-row slab.  Averaged
+    execute).  counts = [apply MFMAs, apply tiles, quad Grams, of which on 2
+    bf16 parts] summed over ranks: one v_mfma_f32_32x32x16_bf16 = 32768 flops;
+    an apply tile is 32 rows x 256 columns of A or V read and written (64 KiB);
+    a quad Gram reads 256 columns of m_pad rows and issues 288 MFMAs (in
+    32x32x16 units) per 32-row slab, 144 on 2 parts.  Averaged
     over the whole time to converge, so these are lower bounds on the quad
     kernels' own rates (the EVD chain and the single steps that open each
     sweep are in the time but not in the counts)."""
-    mf_apply, tiles, gq = counts
-    mf_gram = gq * (m_pad / 32.0) * 288.0
+    mf_apply, tiles, gq, gq2 = counts
+    mf_gram = (gq - gq2) * (m_pad / 32.0) * 288.0 + gq2 * (m_pad / 32.0) * 144.0
     flops = (mf_apply + mf_gram) * 32768.0
     nbytes = tiles * 65536.0 + gq * m_pad * 256.0 * 4.0
     if seconds <= 0 or flops <= 0:
@@ -546,7 +547,8 @@ def work_estimate(counts, m_pad, seconds):
             "executed_mfma_tflops": round(flops / seconds / 1e12, 1),
             "hbm_gb_per_solve": round(nbytes / 1e9, 1),
             "hbm_tb_per_s": round(nbytes / seconds / 1e12, 3),
-            "apply_mfma": int(mf_apply), "apply_tiles": int(tiles), "quad_grams": int(gq)}
+            "apply_mfma": int(mf_apply), "apply_tiles": int(tiles), "quad_grams": int(gq),
+            "quad_grams_2part": int(gq2)}
 
 
 def want_sigma(a, n) -> bool:
@@ -722,7 +724,8 @@ def main():
     # (apply MFMAs and tiles counted on the device, quad Grams on the host)
     wk = last.info.get("work") or {}
     wt = torch.tensor([float(wk.get("apply_mfma", 0)), float(wk.get("apply_tiles", 0)),
-                       float(wk.get("gram_quads", 0))], dtype=torch.float64, device=comm.device)
+                       float(wk.get("gram_quads", 0)), float(wk.get("gram_quads2", 0))],
+                      dtype=torch.float64, device=comm.device)
     comm.allreduce_sum_(wt)
     work_est = work_estimate(wt.cpu().tolist(), int(wk.get("m_pad", m)), ms / 1e3)
     if comm.rank == 0:

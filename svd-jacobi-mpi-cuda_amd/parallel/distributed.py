@@ -318,7 +318,7 @@ class DistributedBlockJacobi(Solver):
         # work actually done by the quad kernels (bench.py's executed-MFMA and
         # HBM estimates): device counters of the apply, summed per sweep without
         # a host sync, and the quad Grams issued
-        work = {"gram_quads": 0}
+        work = {"gram_quads": 0, "gram_quads2": 0}
         work_acc = torch.zeros(2, dtype=torch.float64, device=metric.device)
         if pipelined:
             ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
@@ -326,7 +326,9 @@ class DistributedBlockJacobi(Solver):
 
             def run_steps(pairs, modes, slot):
                 # quads of the quad steps issued (each runs the quad Gram): host count
-                work["gram_quads"] += sum(1 for x in modes if int(x) == 4) * (pairs.shape[1] // 2)
+                nq = sum(1 for x in modes if int(x) == 4) * (pairs.shape[1] // 2)
+                work["gram_quads"] += nq
+                work["gram_quads2"] += nq if gram_parts[0] == 2 else 0
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
                               inner_order=inner, gram_parts=gram_parts[0])
@@ -412,7 +414,8 @@ class DistributedBlockJacobi(Solver):
         t_total = time.perf_counter() - t0
         wa = work_acc.cpu()
         info_work = {"apply_mfma": int(wa[0]) * 24, "apply_tiles": int(wa[1]),
-                     "gram_quads": int(work["gram_quads"]), "m_pad": m_pad}
+                     "gram_quads": int(work["gram_quads"]),
+                     "gram_quads2": int(work["gram_quads2"]), "m_pad": m_pad}
         info = {"tol": tol, "converged": converged, "stop_reason": stop_reason, "work": info_work,
                 "stop_rule": cfg.stop_rule, "dtype": str(pdtype), "geometry": geo, "mma": mma,
                 "inner_order": inner, "quad": quad, "merged_chains": bool(pipelined and merged),
