@@ -256,3 +256,42 @@ def test_local_communicator_is_world_one():
     assert (c.rank, c.world, c.distributed) == (0, 1, False)
     t = torch.arange(6.0)
     assert torch.equal(c.ordered_sum_(t.clone()), t) and c.max_over_ranks(2.5) == 2.5
+
+
+def test_quad_gram_parts_follow_the_rotation_count(monkeypatch):
+    """The quad Gram runs on 2 bf16 parts while the previous sweep rotated
+    every block pair (and in the first sweep), on 3 parts afterwards; SVDJ_DEBUG
+    gram2=0 keeps 3 parts throughout (parallel/distributed.py; libsvdj_dist has
+    the same rule).  The CPU emulation keeps the exact Gram, so both runs give
+    the same result -- here only the requests are checked."""
+    from svdj.ops import kernels as K
+    from svdj.parallel import Communicator, DistributedBlockJacobi
+
+    A = torch.rand(512, 512, generator=torch.Generator().manual_seed(0))
+    cfg = svdj.SolverConfig(dtype=torch.float32, block=64, quad="on", mma="bf16x6")
+    orig = K.block_steps
+    runs = {}
+    for dbg in (None, "gram2=0"):
+        if dbg is None:
+            monkeypatch.delenv("SVDJ_DEBUG", raising=False)
+        else:
+            monkeypatch.setenv("SVDJ_DEBUG", dbg)
+        calls = []
+
+        def wrap(*a, **kw):
+            calls.append(kw.get("gram_parts", 3))
+            return orig(*a, **kw)
+
+        monkeypatch.setattr(K, "block_steps", wrap)
+        res = DistributedBlockJacobi(cfg, Communicator.local("cpu")).solve(A)
+        runs[dbg] = (calls, res)
+    calls, res = runs[None]
+    assert res.info["quad"]
+    n2 = calls.count(2)
+    assert calls[0] == 2 and 0 < n2 < len(calls)
+    assert calls == [2] * n2 + [3] * (len(calls) - n2), calls  # one switch, never back
+    work = res.info["work"]
+    assert 0 < work["gram_quads2"] < work["gram_quads"]
+    calls0, res0 = runs["gram2=0"]
+    assert set(calls0) == {3} and res0.info["work"]["gram_quads2"] == 0
+    assert res0.sweeps == res.sweeps and torch.equal(res0.S, res.S)
