@@ -3330,16 +3330,22 @@ extern "C" int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_p
 // slabs (3P x nchunk x W x W): [0, P) the pairs' Grams, then C_ad, C_bc, C_ab,
 // C_cd of every quad (gram_quad_kernel).
 extern "C" int svdj_gram_quad(const void* A, int lda, int m_pad, const int32_t* pairs, int P,
-                              int rows_per_chunk, void* slabs, void* stream) {
+                              int rows_per_chunk, void* slabs, int parts, void* stream) {
   if (m_pad <= 0 || m_pad % SVDJ_ROW_ALIGN || lda < m_pad || lda % 4 || P <= 0 || P % 2 ||
-      rows_per_chunk <= 0 || rows_per_chunk % SVDJ_ROW_ALIGN) {
-    set_error("svdj_gram_quad: bad m_pad/lda/P/rows %d/%d/%d/%d", m_pad, lda, P, rows_per_chunk);
+      rows_per_chunk <= 0 || rows_per_chunk % SVDJ_ROW_ALIGN || (parts != 2 && parts != 3)) {
+    set_error("svdj_gram_quad: bad m_pad/lda/P/rows/parts %d/%d/%d/%d/%d", m_pad, lda, P,
+              rows_per_chunk, parts);
     return -2;
   }
   const int nchunk = (m_pad + rows_per_chunk - 1) / rows_per_chunk;
-  hipLaunchKernelGGL(gram_quad_kernel<0>, dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
-                     (hipStream_t)stream, (const float*)A, lda, m_pad, pairs, P, rows_per_chunk,
-                     (float*)slabs);
+  if (parts == 2)
+    hipLaunchKernelGGL((gram_quad_kernel<0, 2>), dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
+                       (hipStream_t)stream, (const float*)A, lda, m_pad, pairs, P, rows_per_chunk,
+                       (float*)slabs);
+  else
+    hipLaunchKernelGGL((gram_quad_kernel<0, 3>), dim3(P / 2, nchunk), dim3(kGramQThreads), 0,
+                       (hipStream_t)stream, (const float*)A, lda, m_pad, pairs, P, rows_per_chunk,
+                       (float*)slabs);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("svdj_gram_quad launch: %s", hipGetErrorString(e));

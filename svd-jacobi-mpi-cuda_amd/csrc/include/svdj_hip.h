@@ -112,9 +112,10 @@ int svdj_gram_cross(int dtype, int W, const void* A, int lda, int m_pad,
                     const int32_t* pairs, int P, int rows_per_chunk, void* slabs, void* stream);
 // The six cross Grams of a quad step (fp32, W = 64; pairs in quad order,
 // P even): slabs (3P x nchunk x W x W) = the P pairs' Grams, then C_ad, C_bc,
-// C_ab, C_cd of every quad.
+// C_ab, C_cd of every quad.  parts: 3 (exact to 2^-26) or 2 (2^-16, the
+// early-sweep Gram of svdj_block_steps' mma bit 8).
 int svdj_gram_quad(const void* A, int lda, int m_pad, const int32_t* pairs, int P,
-                   int rows_per_chunk, void* slabs, void* stream);
+                   int rows_per_chunk, void* slabs, int parts, void* stream);
 // X <- X Q for one pair of column blocks (X = 2W columns, leading dimension
 // ld, `rows` a multiple of SVDJ_ROW_ALIGN), Q row-major 2W x 2W on the
 // device, with matrix-core mode `mma` (as svdj_block_steps).

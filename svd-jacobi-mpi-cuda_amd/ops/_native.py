@@ -125,7 +125,7 @@ def hip_lib():
         _sig(lib, "svdj_gram_cross", c_int,
              [c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_gram_quad", c_int,
-             [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
+             [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p])
         _sig(lib, "svdj_apply_q", c_int,
              [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p])
         _sig(lib, "svdj_set_identity", c_int,

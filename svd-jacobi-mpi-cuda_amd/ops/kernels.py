@@ -382,11 +382,12 @@ def gram_cross(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
 
 
 def gram_quad(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
-              rows_per_chunk: int) -> torch.Tensor:
+              rows_per_chunk: int, parts: int = 3) -> torch.Tensor:
     """The six cross Grams of a quad step (fp32, W = 64): ``pairs`` (P, 2) on
     the device in quad order ((a, c), (b, d) per quad).  Returns the slabs
     (3P, nchunk, W, W): the P pairs' Grams, then C_ad, C_bc, C_ab, C_cd of
-    every quad (csrc/hip/block.hip gram_quad_kernel)."""
+    every quad (csrc/hip/block.hip gram_quad_kernel; ``parts`` 2: the
+    early-sweep form on 2 bf16 parts)."""
     _check_layout(At, m_pad)
     if At.dtype != torch.float32 or W != 64:
         raise ValueError("gram_quad: fp32 data, W = 64")
@@ -395,7 +396,8 @@ def gram_quad(At: torch.Tensor, m_pad: int, pairs: torch.Tensor, W: int,
     nchunk = -(-m_pad // rows_per_chunk)
     slabs = torch.empty(3 * P, nchunk, W, W, dtype=At.dtype, device=At.device)
     hip_check(hip_lib().svdj_gram_quad(_ptr(At), At.stride(0), m_pad, _ptr(pairs), P,
-                                       rows_per_chunk, _ptr(slabs), _stream(At)), "gram_quad")
+                                       rows_per_chunk, _ptr(slabs), int(parts), _stream(At)),
+              "gram_quad")
     return slabs
 
 
