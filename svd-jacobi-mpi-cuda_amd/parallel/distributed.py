@@ -319,6 +319,7 @@ class DistributedBlockJacobi(Solver):
         # HBM estimates): device counters of the apply, summed per sweep without
         # a host sync, and the quad Grams issued
         work = {"gram_quads": 0, "gram_quads2": 0}
+        gram_parts = [3]  # bf16 parts of this sweep's quad Grams (set per sweep below)
         work_acc = torch.zeros(2, dtype=torch.float64, device=metric.device)
         if pipelined:
             ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
@@ -347,15 +348,14 @@ class DistributedBlockJacobi(Solver):
         merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
                                                                     k, quad)
         # Quad Gram precision per sweep: while the previous sweep rotated
-        # every pair (far from convergence: the first ~12 of 18 sweeps at
+        # every pair (far from convergence: the first ~12 of 19 sweeps at
         # 16384^2), the couplings only steer rotation angles and the 2-part
-        # Gram (2^-17) does; later sweeps need the exact one.  SVDJ_DEBUG
-        # gram2=0/1 forces it off / on (A/B).
+        # Gram (~2^-16) does; later sweeps need the exact one
+        # (profiles/r6_gram2; libsvdj_dist: the same rule in svdj_dist_solve).
+        # SVDJ_DEBUG gram2=0/1 forces it off / on (A/B).
         nbt = 2 * P * k
         all_pairs = nbt * (nbt - 1) // 2
-        # (libsvdj_dist: the same rule in svdj_dist_solve)
         gram2 = debug_knob("gram2")
-        gram_parts = [3]
         prev_all = start == 0
         for sw in range(start, cfg.max_sweeps):
             use2 = prev_all if gram2 is None else gram2 == 1
