@@ -393,7 +393,7 @@ def run_native(a, dtype, work):
     dcode = 1 if dtype == torch.float64 else 0
     W = a.block or lib.svdj_dist_choose_block(dcode, world, m, n)
     geo = [C.c_int32() for _ in range(4)]
-    check(lib.svdj_dist_geometry(world, m, n, W, *[C.byref(g) for g in geo]), "svdj_dist_geometry")
+    check(lib.svdj_dist_geometry(world, m, n, W, dcode, *[C.byref(g) for g in geo]), "svdj_dist_geometry")
     B, ncols, m_pad, n_v = (g.value for g in geo)
     held0 = (C.c_int32 * 2)()
     check(lib.svdj_dist_initial_held(world, rank, held0), "svdj_dist_initial_held")

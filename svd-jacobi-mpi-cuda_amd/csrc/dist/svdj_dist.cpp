@@ -231,14 +231,30 @@ extern "C" int svdj_dist_comm_destroy(void* comm) {
   return 0;
 }
 
-extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* ncols, int* m_pad,
-                                  int* n_v) {
-  if (world < 1 || m < n || n < 1 || (W != 32 && W != 64)) return fail(-2, "bad geometry args");
+// Size rule of the quad steps (hk = pairs per chain step), shared by the
+// geometry's padding and svdj_dist_issue_rules (models/block.py quad_size_rule).
+static bool quad_size_rule(int hk, int m_pad, int world) {
+  return hk >= 32 || (hk >= 16 && (m_pad >= 16384 || world == 1));
+}
+
+extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int dtype, int* B, int* ncols,
+                                  int* m_pad, int* n_v) {
+  if (world < 1 || m < n || n < 1 || (W != 32 && W != 64) || dtype < 0 || dtype > 2)
+    return fail(-2, "bad geometry args");
   const int q = 4 * world * W;  // B/W even: super-blocks split in halves
-  const int nc = rup(n > q ? n : q, q);
+  int nc = rup(n > q ? n : q, q);
+  const int mp = rup(m, SVDJ_ROW_ALIGN);
+  // quad steps need k = B/W % 4 == 0: a column count that lands on k % 4 == 2
+  // where the quad rule would hold takes one more q of zero columns (<= 6 %
+  // more columns at the sizes the rule admits; quad vs single steps is 20-25 %
+  // per solve).  Not for fp64 (no quad steps).  distributed.py geometry.
+  if (dtype != 1 && W == 64 && svdj_debug_knob("quad_pad", 1) != 0) {
+    const int k = nc / (2 * world * W);
+    if (k % 4 == 2 && quad_size_rule((k + 2) / 2, mp, world)) nc += q;
+  }
   *ncols = nc;
   *B = nc / (2 * world);
-  *m_pad = rup(m, SVDJ_ROW_ALIGN);
+  *m_pad = mp;
   *n_v = rup(nc, SVDJ_ROW_ALIGN);
   return 0;
 }
@@ -675,8 +691,7 @@ extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k
     return fail(-2, "quad steps need fp32, W = 64, a split-bf16 apply and k %% 4 == 0");
   // models/block.py choose_quad, parallel/distributed.py choose_merged
   const int hk = k / 2;
-  *quad = quad_ok && (quad_mode == 1 ||
-                      (quad_mode == 0 && (hk >= 32 || (hk >= 16 && (m_pad >= 16384 || world == 1)))));
+  *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && quad_size_rule(hk, m_pad, world)));
   const int force = svdj_debug_knob("merge", -1);  // A/B only (svdj_debug.h), world 1 only
   *merged = world == 1 && (force >= 0 ? force == 1 : hk >= (*quad ? 16 : 64));
   return 0;

@@ -109,7 +109,7 @@ int run_rank(const Opts& o, int rank, int world, int device) {
   const int m = o.m, n = o.n;
   const int W = o.W ? o.W : svdj_dist_choose_block(dtype, world, m, n);
   int B, ncols, m_pad, n_v;
-  if (svdj_dist_geometry(world, m, n, W, &B, &ncols, &m_pad, &n_v) < 0) {
+  if (svdj_dist_geometry(world, m, n, W, dtype, &B, &ncols, &m_pad, &n_v) < 0) {
     std::fprintf(stderr, "[rank %d] %s\n", rank, svdj_dist_last_error());
     return 1;
   }

@@ -58,7 +58,7 @@ static int run(int m, int n, const std::vector<double>& A0, const std::string& m
   int B = 0;
   int32_t held[2] = {0, 1};
   if (pipe) {  // 2 super-blocks of B columns (even number of W-blocks each), rows padded
-    if (svdj_dist_geometry(1, m, n, W, &B, &ncols, &m_pad, &n_v) < 0 ||
+    if (svdj_dist_geometry(1, m, n, W, dtype, &B, &ncols, &m_pad, &n_v) < 0 ||
         svdj_dist_initial_held(1, 0, held) < 0) {
       std::fprintf(stderr, "svdj error: %s\n", svdj_dist_last_error());
       return 3;

@@ -36,8 +36,12 @@ int svdj_dist_comm_destroy(void* comm);
 
 // Geometry of an m x n problem (m >= n) on `world` GPUs with block width W:
 // n is padded to ncols = a multiple of 4*world*W columns, cut into 2*world
-// super-blocks of B columns (B/W even); row counts padded to 128.
-int svdj_dist_geometry(int world, int m, int n, int W, int* B, int* ncols, int* m_pad, int* n_v);
+// super-blocks of B columns (B/W even); row counts padded to 128.  dtype 0
+// fp32, 1 fp64, 2 bf16: outside fp64, at W = 64, a count that would give
+// k = B/W % 4 == 2 where the quad-step size rule holds is padded by one more
+// 4*world*W so that quad steps (k % 4 == 0) can run.
+int svdj_dist_geometry(int world, int m, int n, int W, int dtype, int* B, int* ncols, int* m_pad,
+                       int* n_v);
 
 // Default block width (models/block.py choose_block): fp32 64 when a GPU
 // holds >= 1024 columns, fp64 64 when m >= 6144 and >= 2048 columns per GPU,

@@ -85,6 +85,13 @@ def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
     return dtype == torch.float32 and W == 64 and mma in ("bf16x6", "bf16x3") and k % 4 == 0
 
 
+def quad_size_rule(hk: int, m_pad: int, P: int) -> bool:
+    """Size part of choose_quad (hk = pairs per chain step), shared with the
+    geometry's padding (DistributedBlockJacobi.geometry; libsvdj_dist
+    quad_size_rule)."""
+    return hk >= 32 or (hk >= 16 and (m_pad >= 16384 or P == 1))
+
+
 def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int = 0) -> bool:
     """Quad steps for config quad="auto", on any number of GPUs: when a chain
     step holds >= 32 pairs (k // 2 >= 32), or >= 16 pairs on columns of at
@@ -107,7 +114,7 @@ def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int
     quad, 50.6 merged-with-exchanges quad, 51.9 merged single, 43.1 default."""
     if not quad_supported(dtype, W, mma, k):
         return False
-    return k // 2 >= 32 or (k // 2 >= 16 and (m_pad >= 16384 or P == 1))
+    return quad_size_rule(k // 2, m_pad, P)
 
 
 def resolve_quad(mode: str, dtype: torch.dtype, W: int, mma: str, k: int, P: int,

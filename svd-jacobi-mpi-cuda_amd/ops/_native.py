@@ -190,7 +190,7 @@ def dist_lib():
         _sig(lib, "svdj_dist_comm_destroy", c_int, [c_void_p])
         _sig(lib, "svdj_dist_id_file", c_int, [c_int, C.c_char_p, c_double, c_void_p, c_size_t])
         _sig(lib, "svdj_dist_geometry", c_int,
-             [c_int, c_int, c_int, c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
+             [c_int, c_int, c_int, c_int, c_int, c_i32_p, c_i32_p, c_i32_p, c_i32_p])
         _sig(lib, "svdj_dist_choose_block", c_int, [c_int, c_int, c_int, c_int])
         _sig(lib, "svdj_dist_initial_held", c_int, [c_int, c_int, c_i32_p])
         _sig(lib, "svdj_dist_solve", c_int, [C.POINTER(DistProblem), c_void_p])

@@ -202,6 +202,28 @@ def test_svd_api_runs_the_pipeline_engine(svdj, cuda):
     assert steps.info["engine"] == "steps" and steps.converged
 
 
+@pytest.mark.parametrize("m,n", [(4500, 4097), (4200, 6000)])
+def test_svd_api_ragged_shapes(svdj, cuda, m, n):
+    """svd() on shapes that are not multiples of the block: 4097 columns pad
+    to whole 64-column blocks (zero columns ride along the quad steps and the
+    merged issue) and a wide input runs transposed; fp64 svdvals as oracle."""
+    A = svdj.utils.inputs.random_dense(m, n, dtype=torch.float32, device=cuda, seed=21)
+    res = svdj.svd(A)
+    assert res.converged and res.info["engine"] == "pipeline" and res.info["quad"], res.info
+    k = min(m, n)
+    assert res.S.shape == (k,) and res.U.shape == (m, k) and res.V.shape == (n, k)
+    ref = torch.linalg.svdvals(A.double().cpu())
+    got = torch.sort(res.S.double().cpu(), descending=True).values
+    assert float((got - ref).abs().max() / ref[0]) < 1e-6
+    # reconstruction (for the transposed solve A V - U S would measure the
+    # orthogonality of the Jacobi side's U' = V, amplified by sigma ratios)
+    rel = float((A - (res.U * res.S) @ res.V.T).norm() / A.norm())
+    assert rel < 1e-5, rel
+    eye = torch.eye(k, device=cuda)
+    assert float((res.V.T @ res.V - eye).abs().max()) < 1e-4
+    assert float((res.U.T @ res.U - eye).abs().max()) < 1e-4
+
+
 def test_svd_quad_without_v_and_bf16(svdj, cuda):
     """Quad steps without V (jobv = NoVec: the apply's V tiles are skipped)
     give bitwise the singular values of the AllVec solve (V never feeds back

@@ -403,6 +403,49 @@ def test_native_issue_rules_match_python(monkeypatch):
             if world > 1:
                 assert not want_m, where
 
+def test_native_geometry_matches_python_and_pads_for_quad_steps():
+    """svdj_dist_geometry and DistributedBlockJacobi.geometry agree on every
+    shape; a column count that would land on k % 4 == 2 where the quad rule
+    holds is padded to the next k % 4 == 0 (4097 columns on one GPU: 68 -> 72
+    blocks, so quad steps run), but not for fp64 (no quad steps) nor where
+    the rule would not take quad steps anyway (small k, short columns at
+    P > 1); multiples of the quad granule are never padded."""
+    import ctypes
+    import itertools
+    import types
+
+    import torch
+
+    from svdj.ops import _native as nat
+    from svdj.parallel import DistributedBlockJacobi
+
+    lib = nat.dist_lib()
+    out = [ctypes.c_int32() for _ in range(4)]
+
+    def native(P, m, n, W, code):
+        assert lib.svdj_dist_geometry(P, m, n, W, code, *[ctypes.byref(o) for o in out]) == 0
+        return tuple(o.value for o in out)
+
+    def python(P, m, n, W, dt):
+        s = DistributedBlockJacobi(svdj.SolverConfig(block=W), types.SimpleNamespace(world=P))
+        g = s.geometry(m, n, dt)
+        return g["B"], g["ncols"], g["m_pad"], g["n_v"]
+
+    dts = ((torch.float32, 0), (torch.float64, 1), (torch.float32, 2))
+    for P, n, W, (dt, code) in itertools.product((1, 2, 4, 8), (100, 2300, 4097, 4352, 8200, 16400,
+                                                                 16384, 33000), (32, 64), dts):
+        for m in (n, 2 * n, 17000):
+            if m < n:
+                continue
+            assert native(P, m, n, W, code) == python(P, m, n, W, dt), (P, m, n, W, code)
+    assert native(1, 4500, 4097, 64, 0)[0] // 64 == 36   # padded: quad steps
+    assert native(1, 4500, 4097, 64, 1)[0] // 64 == 34   # fp64: not padded
+    assert native(1, 16400, 16400, 64, 0)[0] // 64 == 132
+    assert native(1, 4096, 4096, 64, 0)[0] // 64 == 32   # exact granule: unchanged
+    assert native(8, 16384, 16384, 64, 0)[0] // 64 == 16
+    assert native(2, 8200, 8200, 64, 0)[0] // 64 == 34   # 17 pairs, 8192-row columns: no quad
+
+
 def test_quad_and_merge_rules_pin_the_measured_choices():
     """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
     quad steps on 1, 2 and 4 GPUs (64 / 32 / 16 pairs per chain step, 16384
