@@ -1214,7 +1214,8 @@ extern "C" int svdj_dist_solve(svdj_dist_problem* p, void* sigma) {
         const int cz = z.stream;
         SVDJC(svdj_block_steps(h->dtype, W, h->m_pad, p->At, h->m_pad, p->Vt, h->n_v, h->n_v, p->D,
                                dev_pairs(z), z.t->npairs, z.t->steps, z.t->modes.data(), p->tol,
-                               p->tol_mode, 1, h->ws[cz], h->wsb, h->metric, mma_sweep, st[cz]));
+                               p->tol_mode, 1, h->ws[cz], h->wsb, h->metric,
+                               mma_sweep | (h->quad ? 512 : 0), st[cz]));  // bit 9: chains share the GPU
       }
       for (int q = 0; q < n_t; ++q) {
         const Item& x = items[idx[q]];

@@ -2172,6 +2172,15 @@ __global__ __launch_bounds__(NT) void quad_update_kernel(
 // contiguous ranges (one workgroup per CU: the LDS is 160 KB).
 constexpr int kQuadTsThreads = 512;
 constexpr int kQuadTsGrid = 256;
+// While the other chain's latency-bound kernels (Gram, EVDs, Q builds, update)
+// run concurrently on another stream (two-chain issue, every multi-GPU plan),
+// a smaller grid leaves them CUs to start on at once instead of behind the
+// persistent apply's 160 KB-LDS workgroups.  16384^2 rank plans, ms per sweep
+// (profiles/r6_grid): P = 4 (8 quads per apply) 256 WGs 65.5-69.8, 224
+// 64.6-65.3, 208 63.8-65.6, 192 63.4-64.1; P = 2 (16 quads) 256 118.0-125.5,
+// 224 116.4-118.3, 192 118.4-120.7.  The merged one-GPU issue keeps the
+// whole chip.
+__host__ __device__ constexpr int quad_ts_grid_shared(int nq) { return nq <= 8 ? 192 : 224; }
 template <int NP>
 struct QuadTsLds {
   static constexpr int S_BYTES = 16 * NP * SVDJ_WAVE * 16;  // split image of a 32-row tile
@@ -2820,6 +2829,7 @@ struct Chain {
   int32_t* skip2[2];
   hipStream_t st;
   int gram_np;  // bf16 parts of the quad Gram (3; 2 far from convergence)
+  int shared;  // another chain runs concurrently on this GPU (svdj_block_steps mma bit 9)
 };
 
 template <typename T, int W>
@@ -2846,6 +2856,7 @@ static int chain_init(Chain<T>& c, int m_pad, T* A, int lda, T* V, int n_v, int 
   }
   c.m_pad = m_pad; c.lda = lda; c.n_v = n_v; c.ldv = ldv; c.P = P; c.steps = steps;
   c.gram_np = 3;
+  c.shared = 0;
   c.A = A; c.V = V; c.D = D; c.pairs = pairs; c.modes = modes; c.st = st;
   c.g = make_geometry(W, P, m_pad, V ? n_v : 0, mma);
   char* w = (char*)ws;
@@ -3084,12 +3095,15 @@ static int launch_apply(const Chain<T>& c, int s, int mma, uint32_t* metric) {
       uint32_t* work = metric ? metric + 6 : nullptr;
       // cheap k halves: |T - I| <= 2^-7 (A/B only: SVDJ_DEBUG cheap_log2, svdj_debug.h)
       static const float cheap_tol = ldexpf(1.0f, -svdj_debug_knob("cheap_log2", 7));
+      // persistent grid (A/B override: SVDJ_DEBUG apply_grid)
+      static const int grid_knob = svdj_debug_knob("apply_grid", 0);
+      const int grid = grid_knob > 0 ? grid_knob : c.shared ? quad_ts_grid_shared(nq) : kQuadTsGrid;
       if (mma == 1)
-        hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
+        hipLaunchKernelGGL((apply_quad_ts_kernel<3>), dim3(grid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
                            c.skip2[b], work, cheap_tol);
       else
-        hipLaunchKernelGGL((apply_quad_ts_kernel<2>), dim3(kQuadTsGrid), dim3(kQuadTsThreads), 0,
+        hipLaunchKernelGGL((apply_quad_ts_kernel<2>), dim3(grid), dim3(kQuadTsThreads), 0,
                            c.st, c.A, c.lda, at, c.V, c.ldv, vt, pr, nq, c.Ts[b], c.skip1[b],
                            c.skip2[b], work);
       SVDJ_LAUNCH_CHECK();
@@ -3192,11 +3206,13 @@ static int steps_dispatch(int m_pad, void* A, int lda, void* V, int n_v, int ldv
                           uint32_t* metric, int mma, void* stream) {
   Chain<T> c;
   const int gram2 = (mma >> 8) & 1;  // svdj_block_steps' mma bit 8
+  const int shared = (mma >> 9) & 1;  // bit 9
   mma &= 0xff;
   int rc = chain_init<T, W>(c, m_pad, (T*)A, lda, (T*)V, n_v, ldv, (T*)D, pairs, P, steps, modes,
                             ws, ws_bytes, mma, (hipStream_t)stream);
   if (rc) return rc;
   if (gram2) c.gram_np = 2;
+  c.shared = shared;
   return block_steps_t<T, W>(c, tol, absmode, max_inner, metric, mma);
 }
 
@@ -3206,7 +3222,9 @@ extern "C" int svdj_block_steps(int dtype, int W, int m_pad, void* A, int lda, v
                                 void* ws, size_t ws_bytes, uint32_t* metric, int mma,
                                 void* stream) {
   // mma bits 0-7: the apply's matrix-core mode; bit 8: quad Gram with 2 bf16
-  // parts (gram_quad_kernel<0, 2>) for sweeps far from convergence
+  // parts (gram_quad_kernel<0, 2>) for sweeps far from convergence; bit 9:
+  // another chain runs concurrently on this GPU (quad apply on
+  // quad_ts_grid_shared workgroups)
   int rc = check_dims(m_pad, lda, V, n_v, ldv, mma & 0xff);
   if (rc) return rc;
   if (tol_mode != 0 && tol_mode != 1) {

@@ -18,6 +18,8 @@
 //     gram2=0|1            quad Gram on 2 bf16 parts forced off / on (default:
 //                          while the previous sweep rotated every pair; both
 //                          engines: parallel/distributed.py, svdj_dist_solve)
+//     apply_grid=N         quad apply persistent grid (default 256 = one
+//                          workgroup per CU)
 //     quad_pad=0           no extra zero columns for quad steps (both engines'
 //                          geometry: svdj_dist_geometry, distributed.py)
 //

@@ -317,13 +317,15 @@ def check_block(dtype, W):
 
 def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_slot: int = 0,
                 mma="native", pool: dict | None = None, tol_mode="relative",
-                inner_order="cyclic", gram_parts: int = 3):
+                inner_order="cyclic", gram_parts: int = 3, shared_gpu: bool = False):
     """Run ``len(modes)`` block steps on the current stream.  pairs: int32
     (steps, P, 2) on At's device (block indices local to At); modes: list of
     0 (cross) / 1 (full) (see step_modes for ``inner_order``).  Chains running
     concurrently on different streams must use different ``ws_slot`` values.
     ``gram_parts`` 2: the quad Gram on 2 bf16 parts (svdj_block_steps' mma bit
-    8; GPU only, the CPU emulation keeps the exact Gram)."""
+    8; GPU only, the CPU emulation keeps the exact Gram).  ``shared_gpu``:
+    another chain runs concurrently on this GPU (bit 9: the quad apply leaves
+    it a quarter of the CUs)."""
     modes = step_modes(modes, inner_order)
     _check_layout(At, m_pad)
     check_block(At.dtype, W)
@@ -340,7 +342,8 @@ def block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, max_inner, metric, ws_sl
             dtype_code(At.dtype), W, m_pad, _ptr(At), At.stride(0), _ptr(Vt), n_v, ldv,
             _ptr(D), _ptr(pairs), P, steps, md, float(tol), tol_mode_code(tol_mode),
             int(max_inner), _ptr(ws), ws.numel(), _ptr(metric),
-            mma_code(mma, At.dtype) | (256 if gram_parts == 2 else 0), _stream(At)), "block_steps")
+            mma_code(mma, At.dtype) | (256 if gram_parts == 2 else 0) | (512 if shared_gpu else 0),
+            _stream(At)), "block_steps")
     else:
         for s in range(steps):
             if modes[s] == 5:  # second step of a quad: done with its first

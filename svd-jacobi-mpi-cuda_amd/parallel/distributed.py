@@ -330,6 +330,7 @@ class DistributedBlockJacobi(Solver):
         # a host sync, and the quad Grams issued
         work = {"gram_quads": 0, "gram_quads2": 0}
         gram_parts = [3]  # bf16 parts of this sweep's quad Grams (set per sweep below)
+        shared_gpu = [False]  # two chains issued concurrently (set with `merged` below)
         work_acc = torch.zeros(2, dtype=torch.float64, device=metric.device)
         if pipelined:
             ex = PipelineExecutor(comm, streams, At, Vt, D, k, W, tour, timing=cfg.comm_timing,
@@ -342,7 +343,8 @@ class DistributedBlockJacobi(Solver):
                 work["gram_quads2"] += nq if gram_parts[0] == 2 else 0
                 K.block_steps(At, Vt, D, m_pad, pairs, W, modes, tol, cfg.max_inner_sweeps,
                               metric, slot, mma=mma, pool=self._ws, tol_mode=cfg.tol_mode,
-                              inner_order=inner, gram_parts=gram_parts[0])
+                              inner_order=inner, gram_parts=gram_parts[0],
+                              shared_gpu=shared_gpu[0])
         # One rank, no exchanges, >= 64 pairs per chain step (>= 32 with quad
         # steps): the two chains' parallel tasks merged into single launches
         # of twice the pairs (PipelineExecutor.run_merged), the EVD latency
@@ -357,6 +359,9 @@ class DistributedBlockJacobi(Solver):
         # steps, 43.1 not merged; profiles/r6_issue/plan_p8).
         merged = pipelined and dev.type == "cuda" and choose_merged(P if comm.distributed else 1,
                                                                     k, quad)
+        # the two chains on their own streams: the quad apply leaves the other
+        # chain CUs (svdj_block_steps bit 9; libsvdj_dist the same)
+        shared_gpu[0] = pipelined and quad and not (merged and not comm.distributed)
         # Quad Gram precision per sweep: while the previous sweep rotated
         # every pair (far from convergence: the first ~12 of 19 sweeps at
         # 16384^2), the couplings only steer rotation angles and the 2-part
