@@ -234,7 +234,8 @@ extern "C" int svdj_dist_comm_destroy(void* comm) {
 // Size rule of the quad steps (hk = pairs per chain step), shared by the
 // geometry's padding and svdj_dist_issue_rules (models/block.py quad_size_rule).
 static bool quad_size_rule(int hk, int m_pad, int world) {
-  return hk >= 32 || (hk >= 16 && (m_pad >= 16384 || world == 1));
+  (void)m_pad;  // round 6: no row condition since the shared-GPU apply grid (profiles/r6_rule)
+  return hk >= 16 || (hk >= 12 && world > 1);
 }
 
 extern "C" int svdj_dist_geometry(int world, int m, int n, int W, int dtype, int* B, int* ncols,

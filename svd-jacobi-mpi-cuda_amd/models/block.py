@@ -88,14 +88,15 @@ def quad_supported(dtype: torch.dtype, W: int, mma: str, k: int) -> bool:
 def quad_size_rule(hk: int, m_pad: int, P: int) -> bool:
     """Size part of choose_quad (hk = pairs per chain step), shared with the
     geometry's padding (DistributedBlockJacobi.geometry; libsvdj_dist
-    quad_size_rule)."""
-    return hk >= 32 or (hk >= 16 and (m_pad >= 16384 or P == 1))
+    quad_size_rule).  ``m_pad`` no longer enters (round 6, see choose_quad)."""
+    del m_pad
+    return hk >= 16 or (hk >= 12 and P > 1)
 
 
 def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int = 0) -> bool:
     """Quad steps for config quad="auto", on any number of GPUs: when a chain
-    step holds >= 32 pairs (k // 2 >= 32), or >= 16 pairs on columns of at
-    least 16384 rows; off below.
+    step holds >= 16 pairs (k // 2 >= 16), or >= 12 on more than one GPU;
+    off below (quad_size_rule).
 
     Measured on MI355X with the round-5 kernels (one-read split-bf16 quad
     Gram with a swizzled raw image, a wide chunk reduction when it has many
@@ -111,7 +112,13 @@ def choose_quad(dtype: torch.dtype, W: int, mma: str, k: int, P: int, m_pad: int
     merged into single launches (choose_merged) -- 4096^2 123.5 ms merged quad
     vs 127.1 merged single steps vs 135.4 two chains -- so there the row rule
     does not apply; 16384^2 P=8 (8 pairs) stays without: 52.8 ms per sweep
-    quad, 50.6 merged-with-exchanges quad, 51.9 merged single, 43.1 default."""
+    quad, 50.6 merged-with-exchanges quad, 51.9 merged single, 43.1 default.
+    Round 6, after the quad apply left the concurrent chain CUs
+    (profiles/r6_grid, profiles/r6_rule; simulated plans, ms per sweep, quad
+    vs single): 8192^2 P=2 (16 pairs) 23.6 vs 26.6, 12288^2 P=2 (24) 55.4 vs
+    73.8, 12288^2 P=4 (12) 34.7 vs 41.0 -- the row condition is gone; with 8
+    pairs 16384^2 P=8 43.3 vs 43.1, 4096^2 P=2 9.05 vs 8.98, 8192^2 P=4 16.6
+    vs 17.5: still off there."""
     if not quad_supported(dtype, W, mma, k):
         return False
     return quad_size_rule(k // 2, m_pad, P)

@@ -408,8 +408,8 @@ def test_native_geometry_matches_python_and_pads_for_quad_steps():
     shape; a column count that would land on k % 4 == 2 where the quad rule
     holds is padded to the next k % 4 == 0 (4097 columns on one GPU: 68 -> 72
     blocks, so quad steps run), but not for fp64 (no quad steps) nor where
-    the rule would not take quad steps anyway (small k, short columns at
-    P > 1); multiples of the quad granule are never padded."""
+    the rule would not take quad steps anyway (fewer than 12 pairs per step);
+    multiples of the quad granule are never padded."""
     import ctypes
     import itertools
     import types
@@ -443,15 +443,19 @@ def test_native_geometry_matches_python_and_pads_for_quad_steps():
     assert native(1, 16400, 16400, 64, 0)[0] // 64 == 132
     assert native(1, 4096, 4096, 64, 0)[0] // 64 == 32   # exact granule: unchanged
     assert native(8, 16384, 16384, 64, 0)[0] // 64 == 16
-    assert native(2, 8200, 8200, 64, 0)[0] // 64 == 34   # 17 pairs, 8192-row columns: no quad
+    assert native(2, 8200, 8200, 64, 0)[0] // 64 == 36   # 17 -> 18 pairs per step: quad
+    assert native(8, 16400, 16400, 64, 0)[0] // 64 == 18  # 9 pairs: no quad, no padding
 
 
 def test_quad_and_merge_rules_pin_the_measured_choices():
     """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
     quad steps on 1, 2 and 4 GPUs (64 / 32 / 16 pairs per chain step, 16384
     rows) but not on 8 (8 pairs); 8192^2 on one GPU does, merged (32 pairs);
-    4096^2 on one GPU does too, merged (16 pairs: round 6, profiles/r6_issue),
-    but 8192^2 on two GPUs (16 pairs on 8192-row columns) does not."""
+    4096^2 on one GPU does too, merged (16 pairs: round 6, profiles/r6_issue);
+    since the quad apply leaves the concurrent chain CUs (round 6,
+    profiles/r6_grid) quad steps win from 12 pairs per step on columns of any
+    length (8192^2 on two GPUs, 12288^2 on four), not yet at 8 pairs
+    (16384^2 on 8 GPUs, 8192^2 on 4: ties or within 5 %)."""
     import torch
 
     from svdj.models.block import resolve_quad
@@ -468,7 +472,9 @@ def test_quad_and_merge_rules_pin_the_measured_choices():
     assert plan(16384, 4) == (True, False)
     assert plan(16384, 8) == (False, False)
     assert plan(4096, 1) == (True, True)
-    assert plan(8192, 2) == (False, False)
+    assert plan(8192, 2) == (True, False)
+    assert plan(12288, 4) == (True, False)
+    assert plan(8192, 4) == (False, False)
     assert plan(8192, 1) == (True, True)
     assert plan(32768, 8) == (True, False)
     assert not resolve_quad("auto", torch.float64, 64, "native", 128, 1, 16384)
