@@ -694,7 +694,7 @@ extern "C" int svdj_dist_issue_rules(int world, int dtype, int W, int mma, int k
   const int hk = k / 2;
   *quad = quad_ok && (quad_mode == 1 || (quad_mode == 0 && quad_size_rule(hk, m_pad, world)));
   const int force = svdj_debug_knob("merge", -1);  // A/B only (svdj_debug.h), world 1 only
-  *merged = world == 1 && (force >= 0 ? force == 1 : hk >= (*quad ? 16 : 64));
+  *merged = world == 1 && (force >= 0 ? force == 1 : *quad ? (hk >= 16 && hk < 32) : hk >= 64);
   return 0;
 }
 

@@ -49,8 +49,9 @@ from .schedule import distributed_sweep_plan, tournament
 
 def choose_merged(P: int, k: int, quad: bool) -> bool:
     """One-GPU merged issue (PipelineExecutor.run_merged) for k W-blocks per
-    super-block: from 64 pairs per chain step, 16 with quad steps (measured:
-    see the comment at its use in DistributedBlockJacobi._solve).  The
+    super-block: from 64 pairs per chain step; with quad steps from 16 to 31
+    pairs (measured: see the comment at its use in
+    DistributedBlockJacobi._solve).  The
     reference's single-process path rotates one pair per launch
     (main.cu:727-758); this is the opposite end: all of a step's pairs of
     both chains in one launch.
@@ -61,7 +62,8 @@ def choose_merged(P: int, k: int, quad: bool) -> bool:
     force = debug_knob("merge")
     if force is not None:
         return force == 1
-    return k // 2 >= (16 if quad else 64)
+    hk = k // 2
+    return 16 <= hk < 32 if quad else hk >= 64
 
 
 class DistributedBlockJacobi(Solver):
@@ -353,7 +355,12 @@ class DistributedBlockJacobi(Solver):
         # pairs keep the overlapped chains (8192^2 merged +10 %); quad steps
         # of 32 pairs merge well (12288^2 1747 -> 1677 ms, 8192^2 per sweep
         # 39.4 -> 36.9 ms, profiles/r5_quad2), and so do quad steps of 16
-        # pairs (4096^2 135.4 -> 123.5 ms, profiles/r6_issue).  SVDJ_DEBUG merge=0/1
+        # pairs (4096^2 135.4 -> 123.5 ms, profiles/r6_issue).  Since the quad
+        # apply leaves the concurrent chain CUs (profiles/r6_grid), the two
+        # chains beat merging again from 32 quad pairs: 16384^2 3169-3187 ->
+        # 3034 ms (same 19 sweeps, bitwise the same result), 8192^2 30.4 ->
+        # 29.5 ms per sweep; 4096^2 (16 pairs) still merges, 110 vs 120 ms
+        # (profiles/r6_merge).  SVDJ_DEBUG merge=0/1
         # overrides; with exchanges merging was slower at every P (round 6,
         # 16384^2 P = 8: 51.9 ms per sweep merged, 50.6 merged with quad
         # steps, 43.1 not merged; profiles/r6_issue/plan_p8).

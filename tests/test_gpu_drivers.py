@@ -154,7 +154,8 @@ def test_bench_rank_plan_simulation(tmp_path):
 
 def test_merged_issue_is_bitwise_the_two_chain_solve(svdj, cuda, monkeypatch):
     """One GPU, 64 pairs per chain step (16384 columns, W = 64): the merged
-    128-pair launches (PipelineExecutor.run_merged, the default there) give
+    128-pair launches (PipelineExecutor.run_merged; the default there until
+    the shared-GPU apply grid of round 6) give
     bitwise the two-chain result -- same pairs in the same step order and the
     Gram keeps the 64-pair row chunking.  One sweep of a 16384 x 16384 input."""
     from svdj.parallel import Communicator, DistributedBlockJacobi

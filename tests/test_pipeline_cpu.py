@@ -450,8 +450,10 @@ def test_native_geometry_matches_python_and_pads_for_quad_steps():
 def test_quad_and_merge_rules_pin_the_measured_choices():
     """The measured decisions (profiles/r5_quad2): 16384^2 fp32 W = 64 runs
     quad steps on 1, 2 and 4 GPUs (64 / 32 / 16 pairs per chain step, 16384
-    rows) but not on 8 (8 pairs); 8192^2 on one GPU does, merged (32 pairs);
+    rows) but not on 8 (8 pairs); 8192^2 on one GPU does (32 pairs);
     4096^2 on one GPU does too, merged (16 pairs: round 6, profiles/r6_issue);
+    from 32 pairs the one-GPU solve keeps the two chains apart (round 6,
+    profiles/r6_merge: with the shared-GPU apply grid they beat merging);
     since the quad apply leaves the concurrent chain CUs (round 6,
     profiles/r6_grid) quad steps win from 12 pairs per step on columns of any
     length (8192^2 on two GPUs, 12288^2 on four), not yet at 8 pairs
@@ -467,7 +469,7 @@ def test_quad_and_merge_rules_pin_the_measured_choices():
         q = resolve_quad("auto", torch.float32, 64, "bf16x6", k, P, m_pad)
         return q, choose_merged(P, k, q)
 
-    assert plan(16384, 1) == (True, True)
+    assert plan(16384, 1) == (True, False)
     assert plan(16384, 2) == (True, False)
     assert plan(16384, 4) == (True, False)
     assert plan(16384, 8) == (False, False)
@@ -475,6 +477,6 @@ def test_quad_and_merge_rules_pin_the_measured_choices():
     assert plan(8192, 2) == (True, False)
     assert plan(12288, 4) == (True, False)
     assert plan(8192, 4) == (False, False)
-    assert plan(8192, 1) == (True, True)
+    assert plan(8192, 1) == (True, False)
     assert plan(32768, 8) == (True, False)
     assert not resolve_quad("auto", torch.float64, 64, "native", 128, 1, 16384)
